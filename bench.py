@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: Llama-2-7B ZeRO-3 bf16 training throughput (tokens/s) on N MI355X GPUs (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+For N>1 the driver launches one rank per GPU with torch.distributed.run (RCCL over xGMI); this script reads
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment.
+
+Weak scaling: every rank runs the same micro-batch (global_batch = N x micro_batch x GAS sequences of seq_len
+tokens). Synthetic uniform-random token ids, random-init weights of the real Llama-2-7B architecture (no network).
+Each timed step is a full training step: forward, backward, gradient reduce-scatter, fused Adam on the fp32
+partitions and parameter re-partitioning — nothing skipped. Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-13b", "tiny"])
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("DS_BENCH_MB", "4")))
+    ap.add_argument("--gas", type=int, default=1)
+    ap.add_argument("--stage", type=int, default=3)
+    ap.add_argument("--ckpt", action="store_true", help="activation checkpointing (not needed with 288 GB HBM)")
+    ap.add_argument("--local_rank", type=int, default=0)
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.models.llama import LlamaConfig, LlamaForCausalLM, llama2_7b_config, llama2_13b_config
+
+    ds.init_distributed(dist_backend="nccl")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    if args.model == "llama2-7b":
+        cfg = llama2_7b_config(max_position_embeddings=args.seq_len)
+    elif args.model == "llama2-13b":
+        cfg = llama2_13b_config(max_position_embeddings=args.seq_len)
+    else:
+        cfg = LlamaConfig(vocab_size=32000, hidden_size=1024, intermediate_size=2816, num_hidden_layers=4,
+                          num_attention_heads=8, max_position_embeddings=args.seq_len)
+    t0 = time.time()
+    torch.manual_seed(1234)
+    # build directly on the GPU in bf16 (fast init; fp32 masters are created by the ZeRO optimizer)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    with torch.device(dev):
+        model = LlamaForCausalLM(cfg)
+    torch.set_default_dtype(prev)
+    if args.ckpt:
+        model.gradient_checkpointing_enable()
+    n_params = sum(p.numel() for p in model.parameters())
+    log(f"[bench] built {args.model}: {n_params / 1e9:.3f}B params in {time.time() - t0:.1f}s")
+
+    config = {
+        "train_micro_batch_size_per_gpu": args.micro_batch,
+        "gradient_accumulation_steps": args.gas,
+        "steps_per_print": 10**9,
+        "bf16": {"enabled": True},
+        "gradient_clipping": 1.0,
+        "optimizer": {"type": "AdamW", "params": {"lr": 1e-4, "betas": [0.9, 0.95], "eps": 1e-8,
+                                                  "weight_decay": 0.1}},
+        "zero_optimization": {
+            "stage": args.stage,
+            "overlap_comm": True,
+            "contiguous_gradients": True,
+            "reduce_bucket_size": int(2e8),
+            "stage3_prefetch_bucket_size": int(2e8),
+            "stage3_param_persistence_threshold": int(1e5),
+            "stage3_max_live_parameters": int(3e9),
+        },
+    }
+    engine, _, _, _ = ds.initialize(model=model, config=config)
+    log(f"[bench] engine ready in {time.time() - t0:.1f}s; mem {torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    batches = [torch.randint(0, cfg.vocab_size, (args.micro_batch, args.seq_len), device=dev, generator=g)
+               for _ in range(2)]
+
+    def train_step(i):
+        for a in range(args.gas):
+            x = batches[(i + a) % 2]
+            loss = engine(x, labels=x)
+            engine.backward(loss)
+            engine.step()
+        return loss
+
+    for i in range(args.warmup):
+        tw = time.time()
+        loss = train_step(i)
+        torch.cuda.synchronize()
+        log(f"[bench] warmup {i}: loss={float(loss):.4f} {time.time() - tw:.2f}s "
+            f"peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+
+    dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        loss = train_step(i)
+        if rank == 0 and (i + 1) % max(1, args.steps // 5) == 0:
+            log(f"[bench] step {i + 1}/{args.steps}")
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    tokens_per_step = world * args.micro_batch * args.gas * args.seq_len
+    tok_s = tokens_per_step * args.steps / elapsed
+    flops_tok = cfg.flops_per_token(args.seq_len)
+    tflops_gpu = tok_s * flops_tok / world / 1e12
+    peak_mem = torch.cuda.max_memory_allocated() / 2**30
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec Llama-2-7B ZeRO-3 at 1/2/4/8 MI355X; peak trainable params/GPU",
+            "value": round(tok_s, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random token ids, random-init weights)",
+            "config": {
+                "model": {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "tiny": "llama-tiny"}[args.model],
+                "global_batch": world * args.micro_batch * args.gas,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{world}",
+                "zero_stage": args.stage,
+                "micro_batch_per_gpu": args.micro_batch,
+                "gradient_accumulation_steps": args.gas,
+                "activation_checkpointing": bool(args.ckpt),
+                "optimizer": "FusedAdam(AdamW, gfx950 kernel)",
+            },
+            "tokens_per_sec_per_gpu": round(tok_s / world, 2),
+            "model_tflops_per_gpu": round(tflops_gpu, 1),
+            "mfu_vs_2.5PF_bf16_dense": round(tflops_gpu / 2500.0, 4),
+            "params": n_params,
+            "peak_mem_gib_per_gpu": round(peak_mem, 1),
+            "final_loss": round(float(loss), 4),
+        }
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

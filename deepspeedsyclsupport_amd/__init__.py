@@ -1,0 +1,113 @@
+"""deepspeedsyclsupport_amd — an MI355X-native (gfx950 / ROCm / RCCL-over-xGMI) ZeRO training & inference framework
+with the capabilities and user API of DeepSpeed (`deepspeed.initialize`, `engine.backward/step`, `zero.Init`,
+`init_inference`, ...). See SURVEY.md for the component map and README.md for the design."""
+__version__ = "0.1.0"
+__version_major__, __version_minor__, __version_patch__ = 0, 1, 0
+__git_hash__ = None
+__git_branch__ = None
+
+import torch  # noqa: E402
+
+from . import comm  # noqa: E402,F401
+from . import comm as dist  # noqa: E402,F401
+from .accelerator import get_accelerator  # noqa: E402,F401
+from .comm import init_distributed  # noqa: E402,F401
+from .runtime import zero  # noqa: E402,F401
+from .runtime.config import DeepSpeedConfig, DeepSpeedConfigError  # noqa: E402,F401
+from .runtime.engine import DeepSpeedEngine  # noqa: E402,F401
+from .runtime.lr_schedules import add_tuning_arguments  # noqa: E402,F401
+from .utils.logging import log_dist, logger  # noqa: E402,F401
+
+
+def _parse_version(s):
+    return tuple(int(x) for x in s.split(".")[:3])
+
+
+def initialize(args=None, model=None, optimizer=None, model_parameters=None, training_data=None, lr_scheduler=None,
+               mpu=None, dist_init_required=None, collate_fn=None, config=None, config_params=None):
+    """Build the training engine (reference `deepspeed/__init__.py:64-202`).
+
+    Returns (engine, optimizer, training_dataloader, lr_scheduler)."""
+    log_dist(f"DeepSpeed-AMD info: version={__version__}", ranks=[0])
+    assert model is not None, "deepspeed.initialize requires a model"
+    zero.partition_parameters.shutdown_init_context()
+    if config is None and config_params is not None:
+        config = config_params
+    if config is None and args is not None:
+        config = getattr(args, "deepspeed_config", None)
+    assert config is not None, "DeepSpeed requires --deepspeed_config or config=..."
+    if dist_init_required is not False:
+        init_distributed(dist_init_required=dist_init_required)
+    cfg = config if isinstance(config, DeepSpeedConfig) else DeepSpeedConfig(config, mpu)
+    pipe = False
+    try:
+        from .runtime.pipe.module import PipelineModule
+        pipe = isinstance(model, PipelineModule)
+    except Exception:
+        pipe = False
+    if pipe:
+        from .runtime.pipe.engine import PipelineEngine
+        engine = PipelineEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
+                                training_data=training_data, lr_scheduler=lr_scheduler, mpu=model.mpu(),
+                                dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
+                                config_class=cfg)
+    elif cfg.hybrid_engine.enabled:
+        from .runtime.hybrid_engine import DeepSpeedHybridEngine
+        engine = DeepSpeedHybridEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
+                                       training_data=training_data, lr_scheduler=lr_scheduler, mpu=mpu,
+                                       dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
+                                       config_class=cfg)
+    else:
+        engine = DeepSpeedEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
+                                 training_data=training_data, lr_scheduler=lr_scheduler, mpu=mpu,
+                                 dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
+                                 config_class=cfg)
+    return engine, engine.optimizer, engine.training_dataloader, engine.lr_scheduler
+
+
+def _add_core_arguments(parser):
+    group = parser.add_argument_group("DeepSpeed", "DeepSpeed configurations")
+    group.add_argument("--deepspeed", default=False, action="store_true", help="Enable DeepSpeed")
+    group.add_argument("--deepspeed_config", default=None, type=str, help="DeepSpeed json configuration file.")
+    group.add_argument("--deepscale", default=False, action="store_true", help=argparse_suppress())
+    group.add_argument("--deepscale_config", default=None, type=str, help=argparse_suppress())
+    group.add_argument("--deepspeed_mpi", default=False, action="store_true",
+                       help="Run via MPI, this will attempt to discover the necessary variables to initialize "
+                       "torch distributed from the MPI environment")
+    return parser
+
+
+def argparse_suppress():
+    import argparse
+    return argparse.SUPPRESS
+
+
+def add_config_arguments(parser):
+    return _add_core_arguments(parser)
+
+
+def default_inference_config():
+    from .inference.config import DeepSpeedInferenceConfig
+    return DeepSpeedInferenceConfig().model_dump()
+
+
+def init_inference(model, config=None, **kwargs):
+    """Inference engine with kernel injection / AutoTP (reference `deepspeed/__init__.py:269-344`)."""
+    from .inference.config import DeepSpeedInferenceConfig
+    from .inference.engine import InferenceEngine
+    if config is None:
+        config = {}
+    if isinstance(config, str):
+        import json
+        with open(config) as f:
+            config = json.load(f)
+    if isinstance(config, dict):
+        overlap = set(config) & set(kwargs)
+        for k in overlap:
+            if config[k] != kwargs[k]:
+                raise ValueError(f"Conflicting argument '{k}' in 'config':{config[k]} and kwargs:{kwargs[k]}")
+        config = {**config, **kwargs}
+        ds_inference_config = DeepSpeedInferenceConfig(**config)
+    else:
+        ds_inference_config = config
+    return InferenceEngine(model, config=ds_inference_config)

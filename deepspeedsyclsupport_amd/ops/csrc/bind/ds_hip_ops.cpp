@@ -1,0 +1,372 @@
+// PyTorch bindings for the gfx950 kernel library (one extension, `ds_hip_ops`).
+// Host-only C++ (compiled with g++ against torch headers); device code lives in the *.hip objects linked in, which
+// expose a C ABI taking raw pointers + hipStream_t. Every op launches on torch's current HIP stream, so ops compose
+// with torch streams, events and hipGraph capture.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime_api.h>
+
+#include <optional>
+#include <vector>
+
+extern "C" {
+int ds_adam_flat(void*, void*, void*, const void*, void*, int64_t, int, int, int, float, float, float, float, float,
+                 float, float, float, int, hipStream_t);
+int ds_adam_multi(void**, void**, void**, const void**, void**, const int64_t*, int, int, int, int, float, float,
+                  float, float, float, float, float, float, int, hipStream_t);
+int ds_lion_flat(void*, void*, const void*, void*, int64_t, int, int, int, float, float, float, float, float,
+                 hipStream_t);
+int ds_adagrad_flat(void*, void*, const void*, void*, int64_t, int, int, int, float, float, float, float, hipStream_t);
+int ds_lamb_flat(void*, void*, void*, const void*, void*, float*, float*, float*, int64_t, int, int, int, float,
+                 float, float, float, float, float, float, float, float, float, hipStream_t);
+int ds_sumsq_multi(const void**, const int64_t*, const int*, int, float*, int, float*, hipStream_t);
+int ds_norm_bwd_blocks(int64_t);
+int ds_rms_fwd(const void*, const void*, const void*, void*, void*, float*, int64_t, int, float, int, hipStream_t);
+int ds_rms_bwd(const void*, const void*, const void*, const float*, const void*, void*, void*, float*, int64_t, int,
+               int, hipStream_t);
+int ds_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int64_t, int, float,
+              int, hipStream_t);
+int ds_ln_bwd(const void*, const void*, const void*, const float*, const float*, const void*, void*, void*, void*,
+              float*, int64_t, int, int, hipStream_t);
+int ds_gated_act_fwd(const void*, void*, int64_t, int, int, int, hipStream_t);
+int ds_gated_act_bwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+int ds_bias_act_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+int ds_bias_act_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+int ds_bias_residual(const void*, const void*, const void*, void*, int64_t, int, float, int, hipStream_t);
+int ds_qkv_rope_fwd(const void*, void*, void*, void*, const float*, const float*, const int*, int, int, int, int, int,
+                    int, int, int, hipStream_t);
+int ds_qkv_rope_bwd(const void*, const void*, const void*, void*, const float*, const float*, const int*, int, int,
+                    int, int, int, int, int, int, hipStream_t);
+int ds_rope_inplace(void*, int, int, int, int, int64_t, int64_t, int64_t, const float*, const float*, const int*, int,
+                    int, int, int, int, hipStream_t);
+int ds_xent_fwd(const void*, const int64_t*, float*, float*, int64_t, int, int64_t, int, float, int, hipStream_t);
+int ds_xent_bwd(const void*, const int64_t*, const float*, const float*, float, void*, int64_t, int, int64_t, int64_t,
+                int, float, int, hipStream_t);
+}
+
+using torch::Tensor;
+using OptT = std::optional<Tensor>;
+
+namespace {
+
+int dcode(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+void check(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " failed: ", hipGetErrorString((hipError_t)rc));
+}
+void need(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void* ptr_or_null(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
+
+// ------------------------------------------------------------------------------------------ optimizers
+void adam_flat(Tensor p, Tensor m, Tensor v, Tensor g, OptT lp, double lr, double b1, double b2, double eps, double wd,
+               double bc1, double bc2, double grad_scale, bool adamw) {
+  need(p, "p"); need(m, "m"); need(v, "v"); need(g, "g");
+  TORCH_CHECK(m.numel() == p.numel() && v.numel() == p.numel() && g.numel() == p.numel(), "adam_flat: size mismatch");
+  TORCH_CHECK(m.scalar_type() == p.scalar_type() && v.scalar_type() == p.scalar_type(), "m/v must match p dtype");
+  int lpd = -1;
+  if (lp.has_value()) { need(*lp, "lp"); TORCH_CHECK(lp->numel() == p.numel(), "lp size"); lpd = dcode(*lp); }
+  check(ds_adam_flat(p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), ptr_or_null(lp), p.numel(), dcode(p),
+                     dcode(g), lpd, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, adamw ? 1 : 0, stream()),
+        "adam_flat");
+}
+
+void adam_multi(std::vector<Tensor> p, std::vector<Tensor> m, std::vector<Tensor> v, std::vector<Tensor> g,
+                std::vector<Tensor> lp, double lr, double b1, double b2, double eps, double wd, double bc1, double bc2,
+                double grad_scale, bool adamw) {
+  const size_t n = p.size();
+  if (n == 0) return;
+  TORCH_CHECK(m.size() == n && v.size() == n && g.size() == n && (lp.empty() || lp.size() == n), "list sizes");
+  std::vector<void*> pp(n), mp(n), vp(n), lpp(lp.empty() ? 0 : n);
+  std::vector<const void*> gp(n);
+  std::vector<int64_t> nn(n);
+  const int pd = dcode(p[0]), gd = dcode(g[0]), ld = lp.empty() ? -1 : dcode(lp[0]);
+  for (size_t i = 0; i < n; ++i) {
+    need(p[i], "p"); need(m[i], "m"); need(v[i], "v"); need(g[i], "g");
+    TORCH_CHECK(dcode(p[i]) == pd && dcode(g[i]) == gd, "adam_multi: mixed dtypes within one call");
+    TORCH_CHECK(m[i].numel() == p[i].numel() && v[i].numel() == p[i].numel() && g[i].numel() == p[i].numel(),
+                "adam_multi: size mismatch");
+    pp[i] = p[i].data_ptr(); mp[i] = m[i].data_ptr(); vp[i] = v[i].data_ptr(); gp[i] = g[i].data_ptr();
+    nn[i] = p[i].numel();
+    if (!lp.empty()) { need(lp[i], "lp"); lpp[i] = lp[i].data_ptr(); }
+  }
+  check(ds_adam_multi(pp.data(), mp.data(), vp.data(), gp.data(), lp.empty() ? nullptr : lpp.data(), nn.data(), (int)n,
+                      pd, gd, ld, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, adamw ? 1 : 0, stream()),
+        "adam_multi");
+}
+
+void lion_flat(Tensor p, Tensor m, Tensor g, OptT lp, double lr, double b1, double b2, double wd, double grad_scale) {
+  need(p, "p"); need(m, "m"); need(g, "g");
+  TORCH_CHECK(m.numel() == p.numel() && g.numel() == p.numel(), "lion_flat: size mismatch");
+  check(ds_lion_flat(p.data_ptr(), m.data_ptr(), g.data_ptr(), ptr_or_null(lp), p.numel(), dcode(p), dcode(g),
+                     lp.has_value() ? dcode(*lp) : -1, lr, b1, b2, wd, grad_scale, stream()),
+        "lion_flat");
+}
+
+void adagrad_flat(Tensor p, Tensor s, Tensor g, OptT lp, double lr, double eps, double wd, double grad_scale) {
+  need(p, "p"); need(s, "s"); need(g, "g");
+  TORCH_CHECK(s.numel() == p.numel() && g.numel() == p.numel(), "adagrad_flat: size mismatch");
+  check(ds_adagrad_flat(p.data_ptr(), s.data_ptr(), g.data_ptr(), ptr_or_null(lp), p.numel(), dcode(p), dcode(g),
+                        lp.has_value() ? dcode(*lp) : -1, lr, eps, wd, grad_scale, stream()),
+        "adagrad_flat");
+}
+
+// returns the applied trust ratio (device scalar)
+Tensor lamb_flat(Tensor p, Tensor m, Tensor v, Tensor g, OptT lp, double lr, double b1, double b2, double eps,
+                 double wd, double bc1, double bc2, double grad_scale, double max_coeff, double min_coeff) {
+  need(p, "p"); need(m, "m"); need(v, "v"); need(g, "g");
+  TORCH_CHECK(m.numel() == p.numel() && v.numel() == p.numel() && g.numel() == p.numel(), "lamb_flat: size mismatch");
+  auto fopt = p.options().dtype(at::kFloat);
+  auto u = torch::empty({p.numel()}, fopt);
+  auto partials = torch::empty({2 * 512}, fopt);
+  auto coeff = torch::empty({1}, fopt);
+  check(ds_lamb_flat(p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), ptr_or_null(lp), u.data_ptr<float>(),
+                     partials.data_ptr<float>(), coeff.data_ptr<float>(), p.numel(), dcode(p), dcode(g),
+                     lp.has_value() ? dcode(*lp) : -1, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, max_coeff,
+                     min_coeff, stream()),
+        "lamb_flat");
+  return coeff;
+}
+
+// sum of squares of all tensors (fp32 device scalar), deterministic
+Tensor sumsq_multi(std::vector<Tensor> xs) {
+  TORCH_CHECK(!xs.empty(), "sumsq_multi: empty list");
+  const int cap = 512 * (int)xs.size();
+  auto fopt = xs[0].options().dtype(at::kFloat);
+  auto partials = torch::empty({cap}, fopt);
+  auto out = torch::zeros({}, fopt);
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> ns;
+  std::vector<int> dts;
+  for (auto& x : xs) {
+    need(x, "x");
+    ptrs.push_back(x.data_ptr());
+    ns.push_back(x.numel());
+    dts.push_back(dcode(x));
+  }
+  check(ds_sumsq_multi(ptrs.data(), ns.data(), dts.data(), (int)xs.size(), partials.data_ptr<float>(), cap,
+                       out.data_ptr<float>(), stream()),
+        "sumsq_multi");
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------ norms
+std::vector<Tensor> rms_fwd(Tensor x, OptT r, Tensor w, double eps) {
+  need(x, "x"); need(w, "w");
+  const int H = (int)x.size(-1);
+  const int64_t rows = x.numel() / H;
+  TORCH_CHECK(w.numel() == H && w.scalar_type() == x.scalar_type(), "rms_fwd: weight shape/dtype");
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({rows}, x.options().dtype(at::kFloat));
+  Tensor res;
+  if (r.has_value()) { need(*r, "r"); TORCH_CHECK(r->sizes() == x.sizes(), "residual shape"); res = torch::empty_like(x); }
+  check(ds_rms_fwd(x.data_ptr(), ptr_or_null(r), w.data_ptr(), y.data_ptr(), res.defined() ? res.data_ptr() : nullptr,
+                   rstd.data_ptr<float>(), rows, H, eps, dcode(x), stream()),
+        "rms_fwd");
+  return {y, res.defined() ? res : torch::Tensor(), rstd};
+}
+
+std::vector<Tensor> rms_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, OptT dres) {
+  need(dy, "dy"); need(x, "x"); need(w, "w"); need(rstd, "rstd");
+  const int H = (int)x.size(-1);
+  const int64_t rows = x.numel() / H;
+  auto dx = torch::empty_like(x);
+  auto dw = torch::empty_like(w);
+  const int nb = ds_norm_bwd_blocks(rows);
+  auto part = torch::empty({(int64_t)nb * H}, x.options().dtype(at::kFloat));
+  if (dres.has_value()) need(*dres, "dres");
+  check(ds_rms_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), ptr_or_null(dres),
+                   dx.data_ptr(), dw.data_ptr(), part.data_ptr<float>(), rows, H, dcode(x), stream()),
+        "rms_bwd");
+  return {dx, dw};
+}
+
+std::vector<Tensor> ln_fwd(Tensor x, OptT r, Tensor g, Tensor b, double eps) {
+  need(x, "x"); need(g, "gamma"); need(b, "beta");
+  const int H = (int)x.size(-1);
+  const int64_t rows = x.numel() / H;
+  auto y = torch::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  auto mean = torch::empty({rows}, fo), rstd = torch::empty({rows}, fo);
+  Tensor res;
+  if (r.has_value()) { need(*r, "r"); res = torch::empty_like(x); }
+  check(ds_ln_fwd(x.data_ptr(), ptr_or_null(r), g.data_ptr(), b.data_ptr(), y.data_ptr(),
+                  res.defined() ? res.data_ptr() : nullptr, mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H,
+                  eps, dcode(x), stream()),
+        "ln_fwd");
+  return {y, res.defined() ? res : torch::Tensor(), mean, rstd};
+}
+
+std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, OptT dres) {
+  need(dy, "dy"); need(x, "x");
+  const int H = (int)x.size(-1);
+  const int64_t rows = x.numel() / H;
+  auto dx = torch::empty_like(x);
+  auto dg = torch::empty_like(g), db = torch::empty_like(g);
+  const int nb = ds_norm_bwd_blocks(rows);
+  auto part = torch::empty({(int64_t)nb * 2 * H}, x.options().dtype(at::kFloat));
+  check(ds_ln_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                  ptr_or_null(dres), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), part.data_ptr<float>(), rows, H,
+                  dcode(x), stream()),
+        "ln_bwd");
+  return {dx, dg, db};
+}
+
+// ------------------------------------------------------------------------------------------ activations
+Tensor gated_act_fwd(Tensor gu, int64_t act) {
+  need(gu, "gu");
+  const int I = (int)(gu.size(-1) / 2);
+  const int64_t rows = gu.numel() / (2 * I);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I;
+  auto out = torch::empty(sizes, gu.options());
+  check(ds_gated_act_fwd(gu.data_ptr(), out.data_ptr(), rows, I, (int)act, dcode(gu), stream()), "gated_act_fwd");
+  return out;
+}
+
+Tensor gated_act_bwd(Tensor dout, Tensor gu, int64_t act) {
+  need(dout, "dout"); need(gu, "gu");
+  const int I = (int)(gu.size(-1) / 2);
+  const int64_t rows = gu.numel() / (2 * I);
+  auto dgu = torch::empty_like(gu);
+  check(ds_gated_act_bwd(dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(), rows, I, (int)act, dcode(gu), stream()),
+        "gated_act_bwd");
+  return dgu;
+}
+
+Tensor bias_act_fwd(Tensor x, OptT bias, int64_t act) {
+  need(x, "x");
+  const int C = (int)x.size(-1);
+  auto y = torch::empty_like(x);
+  check(ds_bias_act_fwd(x.data_ptr(), ptr_or_null(bias), y.data_ptr(), x.numel() / C, C, (int)act, dcode(x), stream()),
+        "bias_act_fwd");
+  return y;
+}
+
+Tensor bias_act_bwd(Tensor dy, Tensor x, OptT bias, int64_t act) {
+  need(dy, "dy"); need(x, "x");
+  const int C = (int)x.size(-1);
+  auto dx = torch::empty_like(x);
+  check(ds_bias_act_bwd(dy.data_ptr(), x.data_ptr(), ptr_or_null(bias), dx.data_ptr(), x.numel() / C, C, (int)act,
+                        dcode(x), stream()),
+        "bias_act_bwd");
+  return dx;
+}
+
+Tensor bias_residual(Tensor x, OptT bias, OptT res, double res_scale) {
+  need(x, "x");
+  const int C = (int)x.size(-1);
+  auto y = torch::empty_like(x);
+  check(ds_bias_residual(x.data_ptr(), ptr_or_null(bias), ptr_or_null(res), y.data_ptr(), x.numel() / C, C, res_scale,
+                         dcode(x), stream()),
+        "bias_residual");
+  return y;
+}
+
+// ------------------------------------------------------------------------------------------ rotary
+std::vector<Tensor> qkv_rope_fwd(Tensor qkv, Tensor cos_t, Tensor sin_t, OptT pos, int64_t Hq, int64_t Hk, int64_t rot,
+                                 int64_t pos_offset) {
+  need(qkv, "qkv"); need(cos_t, "cos"); need(sin_t, "sin");
+  TORCH_CHECK(qkv.dim() == 4 && qkv.size(2) == Hq + 2 * Hk, "qkv must be [B,S,Hq+2Hk,D]");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat, "cos/sin tables must be fp32");
+  const int B = (int)qkv.size(0), S = (int)qkv.size(1), D = (int)qkv.size(3);
+  TORCH_CHECK(cos_t.size(-1) == rot / 2, "cos table width must be rot/2");
+  TORCH_CHECK(pos.has_value() || cos_t.size(0) >= S + pos_offset, "rotary table too short");
+  auto q = torch::empty({B, Hq, S, D}, qkv.options());
+  auto k = torch::empty({B, Hk, S, D}, qkv.options());
+  auto v = torch::empty({B, Hk, S, D}, qkv.options());
+  const int* pp = nullptr;
+  if (pos.has_value()) { need(*pos, "pos"); TORCH_CHECK(pos->scalar_type() == at::kInt, "pos int32"); pp = pos->data_ptr<int>(); }
+  check(ds_qkv_rope_fwd(qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cos_t.data_ptr<float>(),
+                        sin_t.data_ptr<float>(), pp, B, S, (int)Hq, (int)Hk, D, (int)rot, (int)pos_offset, dcode(qkv),
+                        stream()),
+        "qkv_rope_fwd");
+  return {q, k, v};
+}
+
+Tensor qkv_rope_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cos_t, Tensor sin_t, OptT pos, int64_t rot,
+                    int64_t pos_offset) {
+  auto dqc = dq.contiguous(), dkc = dk.contiguous(), dvc = dv.contiguous();
+  const int B = (int)dq.size(0), Hq = (int)dq.size(1), S = (int)dq.size(2), D = (int)dq.size(3);
+  const int Hk = (int)dk.size(1);
+  auto dqkv = torch::empty({B, S, Hq + 2 * Hk, D}, dq.options());
+  const int* pp = pos.has_value() ? pos->data_ptr<int>() : nullptr;
+  check(ds_qkv_rope_bwd(dqc.data_ptr(), dkc.data_ptr(), dvc.data_ptr(), dqkv.data_ptr(), cos_t.data_ptr<float>(),
+                        sin_t.data_ptr<float>(), pp, B, S, Hq, Hk, D, (int)rot, (int)pos_offset, dcode(dq), stream()),
+        "qkv_rope_bwd");
+  return dqkv;
+}
+
+void rope_inplace(Tensor x, Tensor cos_t, Tensor sin_t, OptT pos, int64_t rot, int64_t pos_offset, bool interleaved,
+                  bool inverse) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.stride(3) == 1, "x must be a [B,S,H,D] view with unit last stride");
+  const int* pp = pos.has_value() ? pos->data_ptr<int>() : nullptr;
+  check(ds_rope_inplace(x.data_ptr(), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), x.stride(0),
+                        x.stride(1), x.stride(2), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, (int)rot,
+                        (int)pos_offset, interleaved ? 1 : 0, inverse ? 1 : 0, dcode(x), stream()),
+        "rope_inplace");
+}
+
+// ------------------------------------------------------------------------------------------ cross entropy
+std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels, int64_t ignore_index, double smoothing) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N,V] row-major");
+  need(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  const int64_t N = logits.size(0);
+  auto fo = logits.options().dtype(at::kFloat);
+  auto loss = torch::empty({N}, fo), lse = torch::empty({N}, fo);
+  check(ds_xent_fwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), N,
+                    (int)logits.size(1), logits.stride(0), (int)ignore_index, smoothing, dcode(logits), stream()),
+        "xent_fwd");
+  return {loss, lse};
+}
+
+Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, OptT dloss, double dloss_scalar, bool inplace,
+                int64_t ignore_index, double smoothing) {
+  const int64_t N = logits.size(0);
+  Tensor out = inplace ? logits : torch::empty_like(logits);
+  const float* dl = nullptr;
+  Tensor dlc;
+  if (dloss.has_value()) { dlc = dloss->to(at::kFloat).contiguous(); dl = dlc.data_ptr<float>(); }
+  check(ds_xent_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), dl, (float)dloss_scalar,
+                    out.data_ptr(), N, (int)logits.size(1), logits.stride(0), out.stride(0), (int)ignore_index,
+                    smoothing, dcode(logits), stream()),
+        "xent_bwd");
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "deepspeedsyclsupport_amd gfx950 kernels";
+  m.def("adam_flat", &adam_flat);
+  m.def("adam_multi", &adam_multi);
+  m.def("lion_flat", &lion_flat);
+  m.def("adagrad_flat", &adagrad_flat);
+  m.def("lamb_flat", &lamb_flat);
+  m.def("sumsq_multi", &sumsq_multi);
+  m.def("rms_fwd", &rms_fwd);
+  m.def("rms_bwd", &rms_bwd);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("gated_act_fwd", &gated_act_fwd);
+  m.def("gated_act_bwd", &gated_act_bwd);
+  m.def("bias_act_fwd", &bias_act_fwd);
+  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("bias_residual", &bias_residual);
+  m.def("qkv_rope_fwd", &qkv_rope_fwd);
+  m.def("qkv_rope_bwd", &qkv_rope_bwd);
+  m.def("rope_inplace", &rope_inplace);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+}

@@ -1,0 +1,404 @@
+// RMSNorm / LayerNorm forward+backward (optionally fused with the residual add) for CDNA4.
+//
+// Parity: reference training kernels `csrc/transformer/normalize_kernels.cu` (fused_bias_residual_layer_norm,
+// LayerNormBackward1/2) and inference `csrc/transformer/inference/csrc/{layer_norm.cu,rms_norm.cu}`
+// (fused_ln, fused_residual_ln, rms_norm, pre_rms_norm).
+//
+// MI355X design: ONE WAVE PER ROW. A 64-lane wave owns a row; forward keeps it in NV*8 registers per lane
+// (NV = compile-time vectors per lane, hidden <= 8192), so the statistics need only a 64-lane butterfly (no LDS, no
+// __syncthreads) and the row is read from HBM exactly once. 256-thread blocks = 4 rows; every access is 16 B/lane.
+// Backward: pass 1 over the row accumulates the dot products and the per-lane dgamma/dbeta partials, pass 2
+// re-reads the (L1/L2-hot) row to write dx. dgamma/dbeta partials are reduced across the block's 4 waves in LDS
+// and written as one fp32 row per block, then summed by a column kernel (deterministic, no float atomics).
+#include "../include/ds_hip.h"
+
+namespace {
+
+template <typename T, int NV>
+__device__ __forceinline__ void load_row(const T* row, int H, int lane, float (&v)[NV][8]) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < H) Vec8<T>::load(row + c, v[k]);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void zero8(float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+}
+
+// ------------------------------------------------------------------------------------------------ RMSNorm fwd
+template <typename T, int NV, bool RES>
+__global__ void __launch_bounds__(256) rms_fwd_kernel(const T* __restrict__ x, const T* __restrict__ r,
+                                                      const T* __restrict__ w, T* __restrict__ y,
+                                                      T* __restrict__ res_out, float* __restrict__ rstd_out,
+                                                      int64_t rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += wstride) {
+    float v[NV][8];
+    load_row<T, NV>(x + row * H, H, lane, v);
+    if (RES) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < H) {
+          float rr[8];
+          Vec8<T>::load(r + row * H + c, rr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[k][j] += rr[j];
+          Vec8<T>::store(res_out + row * H + c, v[k]);
+        }
+      }
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss = fmaf(v[k][j], v[k][j], ss);
+    ss = wave_sum(ss);
+    const float rs = rsqrtf(ss / H + eps);
+    if (lane == 0 && rstd_out) rstd_out[row] = rs;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float ww[8], o[8];
+        Vec8<T>::load(w + c, ww);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[k][j] * rs * ww[j];
+        Vec8<T>::store(y + row * H + c, o);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ RMSNorm bwd
+// x is the normalized input (x + r when the forward fused the residual). dx (+ dres if given).
+template <typename T, int NV, bool ADD_DRES>
+__global__ void __launch_bounds__(256) rms_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                      const T* __restrict__ w, const float* __restrict__ rstd,
+                                                      const T* __restrict__ dres, T* __restrict__ dx,
+                                                      float* __restrict__ dw_part, int64_t rows, int H) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // [4][H]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float dwacc[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) zero8(dwacc[k]);
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += wstride) {
+    const float rs = rstd[row];
+    const T* xr = x + row * H;
+    const T* gr = dy + row * H;
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float xv[8], gv[8], ww[8];
+        Vec8<T>::load(xr + c, xv);
+        Vec8<T>::load(gr + c, gv);
+        Vec8<T>::load(w + c, ww);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dwacc[k][j] = fmaf(gv[j], xv[j] * rs, dwacc[k][j]);
+          dot = fmaf(gv[j] * ww[j], xv[j], dot);
+        }
+      }
+    }
+    dot = wave_sum(dot);
+    const float c2 = dot * rs * rs * rs / H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float xv[8], gv[8], ww[8], o[8];
+        Vec8<T>::load(xr + c, xv);
+        Vec8<T>::load(gr + c, gv);
+        Vec8<T>::load(w + c, ww);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = gv[j] * ww[j] * rs - xv[j] * c2;
+        if (ADD_DRES) {
+          float d2[8];
+          Vec8<T>::load(dres + row * H + c, d2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += d2[j];
+        }
+        Vec8<T>::store(dx + row * H + c, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < H) {
+      *reinterpret_cast<f32x4*>(&sm[wid * H + c]) = f32x4{dwacc[k][0], dwacc[k][1], dwacc[k][2], dwacc[k][3]};
+      *reinterpret_cast<f32x4*>(&sm[wid * H + c + 4]) = f32x4{dwacc[k][4], dwacc[k][5], dwacc[k][6], dwacc[k][7]};
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += 256)
+    dw_part[(int64_t)blockIdx.x * H + c] = sm[c] + sm[H + c] + sm[2 * H + c] + sm[3 * H + c];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int nb, int H, int ld,
+                                                     T* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= H) return;
+  float acc = 0.f;
+  for (int b = 0; b < nb; ++b) acc += part[(int64_t)b * ld + c];
+  out[c] = (T)acc;
+}
+
+// ------------------------------------------------------------------------------------------------ LayerNorm
+template <typename T, int NV, bool RES>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ r,
+                                                     const T* __restrict__ gamma, const T* __restrict__ beta,
+                                                     T* __restrict__ y, T* __restrict__ res_out,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int64_t rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += wstride) {
+    float v[NV][8];
+    load_row<T, NV>(x + row * H, H, lane, v);
+    if (RES) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < H) {
+          float rr[8];
+          Vec8<T>::load(r + row * H + c, rr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[k][j] += rr[j];
+          Vec8<T>::store(res_out + row * H + c, v[k]);
+        }
+      }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[k][j];
+    const float mu = wave_sum(s) / H;
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[k][j] - mu;
+          ss = fmaf(d, d, ss);
+        }
+      }
+    }
+    const float rs = rsqrtf(wave_sum(ss) / H + eps);
+    if (lane == 0) {
+      if (mean_out) mean_out[row] = mu;
+      if (rstd_out) rstd_out[row] = rs;
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float gg[8], bb[8], o[8];
+        Vec8<T>::load(gamma + c, gg);
+        Vec8<T>::load(beta + c, bb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mu) * rs * gg[j] + bb[j];
+        Vec8<T>::store(y + row * H + c, o);
+      }
+    }
+  }
+}
+
+template <typename T, int NV, bool ADD_DRES>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const T* __restrict__ gamma, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const T* __restrict__ dres,
+                                                     T* __restrict__ dx, float* __restrict__ part, int64_t rows,
+                                                     int H) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // [4][H], used twice (dgamma then dbeta)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float dg[NV][8], db[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) { zero8(dg[k]); zero8(db[k]); }
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += wstride) {
+    const float mu = mean[row], rs = rstd[row];
+    const T* xr = x + row * H;
+    const T* gr = dy + row * H;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float xv[8], gv[8], gm[8];
+        Vec8<T>::load(xr + c, xv);
+        Vec8<T>::load(gr + c, gv);
+        Vec8<T>::load(gamma + c, gm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - mu) * rs;
+          dg[k][j] = fmaf(gv[j], xh, dg[k][j]);
+          db[k][j] += gv[j];
+          const float g = gv[j] * gm[j];
+          s1 += g;
+          s2 = fmaf(g, xh, s2);
+        }
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float xv[8], gv[8], gm[8], o[8];
+        Vec8<T>::load(xr + c, xv);
+        Vec8<T>::load(gr + c, gv);
+        Vec8<T>::load(gamma + c, gm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (gv[j] * gm[j] - s1 - (xv[j] - mu) * rs * s2);
+        if (ADD_DRES) {
+          float d2[8];
+          Vec8<T>::load(dres + row * H + c, d2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += d2[j];
+        }
+        Vec8<T>::store(dx + row * H + c, o);
+      }
+    }
+  }
+  // dgamma partial -> part[b][0:H], dbeta partial -> part[b][H:2H]
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float (&a)[8] = pass == 0 ? dg[k] : db[k];
+        *reinterpret_cast<f32x4*>(&sm[wid * H + c]) = f32x4{a[0], a[1], a[2], a[3]};
+        *reinterpret_cast<f32x4*>(&sm[wid * H + c + 4]) = f32x4{a[4], a[5], a[6], a[7]};
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += 256)
+      part[(int64_t)blockIdx.x * 2 * H + pass * H + c] = sm[c] + sm[H + c] + sm[2 * H + c] + sm[3 * H + c];
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+#define DISPATCH_T(dt, ...)                                    \
+  do {                                                         \
+    if ((dt) == DS_F32) { using T = float; __VA_ARGS__; }      \
+    else if ((dt) == DS_BF16) { using T = bf16; __VA_ARGS__; } \
+    else { using T = fp16; __VA_ARGS__; }                      \
+  } while (0)
+
+// NV buckets: hidden <= 512*NV
+#define DISPATCH_NV(H, ...)                                      \
+  do {                                                           \
+    const int nv__ = ((H) + 511) / 512;                          \
+    if (nv__ <= 1) { constexpr int NV = 1; __VA_ARGS__; }        \
+    else if (nv__ <= 2) { constexpr int NV = 2; __VA_ARGS__; }   \
+    else if (nv__ <= 4) { constexpr int NV = 4; __VA_ARGS__; }   \
+    else if (nv__ <= 6) { constexpr int NV = 6; __VA_ARGS__; }   \
+    else if (nv__ <= 8) { constexpr int NV = 8; __VA_ARGS__; }   \
+    else if (nv__ <= 12) { constexpr int NV = 12; __VA_ARGS__; } \
+    else { constexpr int NV = 16; __VA_ARGS__; }                 \
+  } while (0)
+
+static constexpr int kMaxHidden = 8192;
+static int norm_grid(int64_t rows) { return ds_grid_for((rows + 3) / 4, 1, 256 * 8); }
+
+// Number of fp32 partial rows the backward writes for `rows` (host allocates part[nb][H], [nb][2H] for LN).
+extern "C" int ds_norm_bwd_blocks(int64_t rows) { return ds_grid_for((rows + 3) / 4, 1, 512); }
+
+extern "C" int ds_rms_fwd(const void* x, const void* r, const void* w, void* y, void* res_out, float* rstd,
+                          int64_t rows, int H, float eps, int dtype, hipStream_t s) {
+  if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (rows <= 0) return 0;
+  const int grid = norm_grid(rows);
+  DISPATCH_T(dtype, DISPATCH_NV(H, {
+    if (r)
+      hipLaunchKernelGGL((rms_fwd_kernel<T, NV, true>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)r,
+                         (const T*)w, (T*)y, (T*)res_out, rstd, rows, H, eps);
+    else
+      hipLaunchKernelGGL((rms_fwd_kernel<T, NV, false>), dim3(grid), dim3(256), 0, s, (const T*)x, nullptr,
+                         (const T*)w, (T*)y, nullptr, rstd, rows, H, eps);
+  }));
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ds_rms_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres, void* dx,
+                          void* dw, float* part, int64_t rows, int H, int dtype, hipStream_t s) {
+  if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (rows <= 0) return 0;
+  const int nb = ds_norm_bwd_blocks(rows);
+  const size_t lds = 4 * (size_t)H * sizeof(float);
+  DISPATCH_T(dtype, DISPATCH_NV(H, {
+    if (dres)
+      hipLaunchKernelGGL((rms_bwd_kernel<T, NV, true>), dim3(nb), dim3(256), lds, s, (const T*)dy, (const T*)x,
+                         (const T*)w, rstd, (const T*)dres, (T*)dx, part, rows, H);
+    else
+      hipLaunchKernelGGL((rms_bwd_kernel<T, NV, false>), dim3(nb), dim3(256), lds, s, (const T*)dy, (const T*)x,
+                         (const T*)w, rstd, nullptr, (T*)dx, part, rows, H);
+  }));
+  DS_CHECK_LAUNCH();
+  DISPATCH_T(dtype, hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, s, part, nb, H, H,
+                                       (T*)dw));
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ds_ln_fwd(const void* x, const void* r, const void* g, const void* b, void* y, void* res_out,
+                         float* mean, float* rstd, int64_t rows, int H, float eps, int dtype, hipStream_t s) {
+  if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (rows <= 0) return 0;
+  const int grid = norm_grid(rows);
+  DISPATCH_T(dtype, DISPATCH_NV(H, {
+    if (r)
+      hipLaunchKernelGGL((ln_fwd_kernel<T, NV, true>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)r,
+                         (const T*)g, (const T*)b, (T*)y, (T*)res_out, mean, rstd, rows, H, eps);
+    else
+      hipLaunchKernelGGL((ln_fwd_kernel<T, NV, false>), dim3(grid), dim3(256), 0, s, (const T*)x, nullptr,
+                         (const T*)g, (const T*)b, (T*)y, nullptr, mean, rstd, rows, H, eps);
+  }));
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ds_ln_bwd(const void* dy, const void* x, const void* g, const float* mean, const float* rstd,
+                         const void* dres, void* dx, void* dg, void* db, float* part, int64_t rows, int H, int dtype,
+                         hipStream_t s) {
+  if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (rows <= 0) return 0;
+  const int nb = ds_norm_bwd_blocks(rows);
+  const size_t lds = 4 * (size_t)H * sizeof(float);
+  DISPATCH_T(dtype, DISPATCH_NV(H, {
+    if (dres)
+      hipLaunchKernelGGL((ln_bwd_kernel<T, NV, true>), dim3(nb), dim3(256), lds, s, (const T*)dy, (const T*)x,
+                         (const T*)g, mean, rstd, (const T*)dres, (T*)dx, part, rows, H);
+    else
+      hipLaunchKernelGGL((ln_bwd_kernel<T, NV, false>), dim3(nb), dim3(256), lds, s, (const T*)dy, (const T*)x,
+                         (const T*)g, mean, rstd, nullptr, (T*)dx, part, rows, H);
+  }));
+  DS_CHECK_LAUNCH();
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, s, part, nb, H, 2 * H, (T*)dg);
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, s, part + H, nb, H, 2 * H, (T*)db);
+  });
+  DS_CHECK_LAUNCH();
+  return 0;
+}

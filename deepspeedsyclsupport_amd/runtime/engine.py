@@ -1,0 +1,570 @@
+"""DeepSpeedEngine: the training engine behind `initialize()` (reference `runtime/engine.py:179-3600`).
+
+Same user contract: `loss = engine(batch)`, `engine.backward(loss)`, `engine.step()`, `save_checkpoint`/
+`load_checkpoint` with the reference's file names and top-level keys, `train_batch_size()` & friends.
+
+All precision / ZeRO modes run through `FlatZeroOptimizer` (see `runtime/zero/flat_optimizer.py`): stage 0 (bf16 /
+fp16 / fp32 data parallel), 1, 2 and 3, with fused gfx950 Adam and RCCL collectives on side streams.
+"""
+import os
+import re
+import time
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+
+from .. import comm as dist
+from ..accelerator import get_accelerator
+from ..checkpoint import constants as CK
+from ..parallel import groups
+from ..utils.logging import log_dist, logger
+from ..utils.timer import (BACKWARD_GLOBAL_TIMER, BACKWARD_MICRO_TIMER, FORWARD_GLOBAL_TIMER, FORWARD_MICRO_TIMER,
+                           STEP_GLOBAL_TIMER, STEP_MICRO_TIMER, NoopTimer, SynchronizedWallClockTimer, ThroughputTimer)
+from . import lr_schedules
+from .checkpoint_engine import AsyncCheckpointEngine, TorchCheckpointEngine
+from .config import (ADAGRAD_OPTIMIZER, ADAM_OPTIMIZER, ADAMW_OPTIMIZER, LAMB_OPTIMIZER, LION_OPTIMIZER,
+                     ONEBIT_ADAM_OPTIMIZER, ONEBIT_LAMB_OPTIMIZER, SGD_OPTIMIZER, ZERO_ONE_ADAM_OPTIMIZER,
+                     DeepSpeedConfig)
+from .dataloader import DeepSpeedDataLoader, RepeatingLoader
+from .zero.flat_optimizer import FlatZeroOptimizer
+
+
+def _version():
+    from .. import __version__
+    return __version__
+
+
+class DeepSpeedEngine(nn.Module):
+
+    def __init__(self, args, model, optimizer=None, model_parameters=None, training_data=None, lr_scheduler=None,
+                 mpu=None, dist_init_required=None, collate_fn=None, config=None, config_class=None,
+                 dont_change_device=False):
+        super().__init__()
+        self.dont_change_device = dont_change_device
+        self.client_optimizer = optimizer
+        self.client_lr_scheduler = lr_scheduler
+        self.training_data = training_data
+        self.collate_fn = collate_fn
+        self.mpu = mpu
+        self.global_steps = 0
+        self.global_samples = 0
+        self.micro_steps = 0
+        self.skipped_steps = 0
+        self.gradient_average = True
+        self.warn_unscaled_loss = True
+        self.losses = None
+        self.enable_backward_allreduce = True
+        self.checkpoint_engine = None
+        self._is_gradient_accumulation_boundary = None
+        self.training_dataloader = None
+        self.sparse_tensor_module_names = set()
+        self.acc = get_accelerator()
+
+        if dist_init_required is not False:
+            dist.init_distributed(dist_backend=self.acc.communication_backend_name(),
+                                  dist_init_required=dist_init_required)
+        self._config = config_class if config_class is not None else DeepSpeedConfig(config, mpu)
+        dist.configure(deepspeed_config=self._config)
+        self._set_distributed_vars(args)
+        self._configure_groups()
+
+        self.monitor = None
+        try:
+            from ..monitor.monitor import MonitorMaster
+            self.monitor = MonitorMaster(self._config.monitor_config)
+        except Exception:  # monitor backends are optional
+            self.monitor = None
+
+        self.module = model
+        self._configure_distributed_model(model)
+        self.timers = SynchronizedWallClockTimer() if self.wall_clock_breakdown() else NoopTimer()
+        self.tput_timer = ThroughputTimer(batch_size=self.train_batch_size(), steps_per_output=self.steps_per_print())
+        if training_data is not None:
+            self.training_dataloader = self.deepspeed_io(training_data)
+
+        self.optimizer = None
+        self.basic_optimizer = None
+        self.lr_scheduler = None
+        if model_parameters is None:
+            model_parameters = self.module.parameters()
+        if optimizer is not None or self._config.optimizer_name is not None:
+            self._configure_optimizer(optimizer, model_parameters)
+            self._configure_lr_scheduler(lr_scheduler)
+        elif self.zero_optimization_stage() == 3:
+            # ZeRO-3 inference-style partitioning without an optimizer (reference: DeepSpeedZeRoOffload)
+            self._configure_optimizer(torch.optim.SGD(self.module.parameters(), lr=0.0), model_parameters)
+        self.flops_profiler = None
+        if self._config.flops_profiler_config.enabled:
+            from ..profiling.flops_profiler import FlopsProfiler
+            self.flops_profiler = FlopsProfiler(self.module, ds_engine=self)
+        self._configure_checkpointing()
+        if self._config.print_user_config if hasattr(self._config, "print_user_config") and False else False:
+            self._config.print("DeepSpeedEngine configuration")
+
+    # ============================================================================================ setup
+    def _set_distributed_vars(self, args):
+        self.local_rank = int(os.environ.get("LOCAL_RANK", getattr(args, "local_rank", 0) or 0))
+        if self.acc.device_name() != "cpu" and self.acc.is_available():
+            self.acc.set_device(self.local_rank % max(self.acc.device_count(), 1))
+            self.device = torch.device("cuda", self.acc.current_device())
+        else:
+            self.device = torch.device("cpu")
+        self.world_size = dist.get_world_size()
+        self.global_rank = dist.get_rank()
+
+    def _configure_groups(self):
+        sp = self._config.sequence_parallel_size
+        if self.mpu is not None:
+            groups.mpu = self.mpu
+        elif sp > 1 and groups._get_sequence_parallel_group() is None:
+            groups.initialize_sequence_parallel(sp)
+        self.sequence_parallel_size = groups._get_sequence_parallel_world_size()
+        self.seq_data_parallel_group = groups._get_sequence_data_parallel_group()
+        self.seq_dp_world_size = dist.get_world_size(self.seq_data_parallel_group)
+        self.dp_world_size = groups._get_data_parallel_world_size()
+        self.mp_world_size = groups._get_model_parallel_world_size()
+
+    def _dtype(self):
+        if self.fp16_enabled():
+            return torch.float16
+        if self.bfloat16_enabled():
+            return torch.bfloat16
+        return torch.float32
+
+    def _configure_distributed_model(self, model):
+        already_partitioned = any(hasattr(p, "ds_tensor") for p in model.parameters())
+        dtype = self._dtype()
+        if not already_partitioned:
+            if not self.dont_change_device:
+                model.to(self.device)
+            if dtype != torch.float32:
+                for p in model.parameters():
+                    if p.is_floating_point():
+                        p.data = p.data.to(dtype)
+                for b in model.buffers():
+                    pass  # buffers (e.g. fp32 rope tables) keep their dtype
+            self._broadcast_model()
+
+    @torch.no_grad()
+    def _broadcast_model(self):
+        if dist.get_world_size() == 1:
+            return
+        src = groups._get_broadcast_src_rank()
+        for p in self.module.parameters():
+            if torch.is_tensor(p) and p.numel() > 0:
+                dist.broadcast(p.data, src, group=self.seq_data_parallel_group)
+
+    # ============================================================================================ optimizer
+    def _configure_basic_optimizer(self, model_parameters):
+        name = self._config.optimizer_name
+        params = dict(self._config.optimizer_params or {})
+        params.pop("torch_adam", None)
+        adam_w_mode = params.pop("adam_w_mode", True)
+        if name in (ADAM_OPTIMIZER, ADAMW_OPTIMIZER):
+            from ..ops.adam import FusedAdam
+            if name == ADAMW_OPTIMIZER:
+                adam_w_mode = True
+            elif "adam_w_mode" not in (self._config.optimizer_params or {}):
+                adam_w_mode = True if name == ADAMW_OPTIMIZER else adam_w_mode
+            return FusedAdam(model_parameters, adam_w_mode=adam_w_mode, **params)
+        if name == LAMB_OPTIMIZER:
+            from ..ops.lamb import FusedLamb
+            return FusedLamb(model_parameters, **params)
+        if name == LION_OPTIMIZER:
+            from ..ops.lion import FusedLion
+            return FusedLion(model_parameters, **params)
+        if name == ADAGRAD_OPTIMIZER:
+            return torch.optim.Adagrad(model_parameters, **params)
+        if name == SGD_OPTIMIZER:
+            return torch.optim.SGD(model_parameters, **params)
+        if name in (ONEBIT_ADAM_OPTIMIZER, ZERO_ONE_ADAM_OPTIMIZER, ONEBIT_LAMB_OPTIMIZER):
+            from ..runtime.fp16.onebit import build_onebit_optimizer
+            return build_onebit_optimizer(name, model_parameters, self, params)
+        # any torch.optim class by name
+        cls = getattr(torch.optim, name, None)
+        if cls is None:
+            raise ValueError(f"Unknown optimizer {name}")
+        return cls(model_parameters, **params)
+
+    def _configure_optimizer(self, client_optimizer, model_parameters):
+        if client_optimizer is None:
+            basic = self._configure_basic_optimizer(model_parameters)
+        elif isinstance(client_optimizer, torch.optim.Optimizer):
+            basic = client_optimizer
+        else:
+            basic = client_optimizer(model_parameters)
+        self.basic_optimizer = basic
+        stage = self.zero_optimization_stage()
+        dtype = self._dtype()
+        self.optimizer = FlatZeroOptimizer(basic, self.module, self._config, dp_group=self.seq_data_parallel_group,
+                                           stage=stage, mpu=self.mpu, clip_grad=self.gradient_clipping(),
+                                           dtype=dtype,
+                                           communication_data_type=self._config.communication_data_type,
+                                           zero_config=self._config.zero_config, timers=None,
+                                           gradient_accumulation_steps=self.gradient_accumulation_steps())
+
+    def _configure_lr_scheduler(self, client_lr_scheduler):
+        name = self._config.scheduler_name
+        if name is not None:
+            cls = lr_schedules.SCHEDULERS.get(name) or getattr(torch.optim.lr_scheduler, name)
+            self.lr_scheduler = cls(self.optimizer.optimizer, **(self._config.scheduler_params or {}))
+        elif client_lr_scheduler is not None:
+            self.lr_scheduler = client_lr_scheduler(self.optimizer.optimizer) if callable(client_lr_scheduler) and \
+                not hasattr(client_lr_scheduler, "step") else client_lr_scheduler
+        else:
+            self.lr_scheduler = None
+
+    def _configure_checkpointing(self):
+        self.checkpoint_engine = AsyncCheckpointEngine() if self._config.nebula_config.get("enabled", False) \
+            else TorchCheckpointEngine()
+        self.save_non_zero_checkpoint = dist.get_rank(self.seq_data_parallel_group) == 0 or \
+            self.zero_optimization_stage() == 3
+        self.save_zero_checkpoint = self.optimizer is not None
+
+    # ============================================================================================ config accessors
+    @property
+    def config(self):
+        return self._config.param_dict
+
+    def train_batch_size(self):
+        return self._config.train_batch_size
+
+    def train_micro_batch_size_per_gpu(self):
+        return self._config.train_micro_batch_size_per_gpu
+
+    def gradient_accumulation_steps(self):
+        return self._config.gradient_accumulation_steps
+
+    def set_train_batch_size(self, train_batch_size):
+        if train_batch_size % (self.train_micro_batch_size_per_gpu() * self.dp_world_size) != 0:
+            raise ValueError("Train batch size must be divisible by micro-batch data parallelism")
+        new_gas = train_batch_size // (self.train_micro_batch_size_per_gpu() * self.dp_world_size)
+        self._config.train_batch_size = train_batch_size
+        self._config.gradient_accumulation_steps = new_gas
+        if self.optimizer is not None:
+            self.optimizer.gas = new_gas
+
+    def steps_per_print(self):
+        return self._config.steps_per_print
+
+    def zero_optimization(self):
+        return self._config.zero_enabled
+
+    def zero_optimization_stage(self):
+        return self._config.zero_optimization_stage
+
+    def zero_optimization_partition_gradients(self):
+        return self.zero_optimization_stage() >= 2
+
+    def zero_optimization_partition_weights(self):
+        return self.zero_optimization_stage() >= 3
+
+    def zero_offload_optimizer(self):
+        return self._config.zero_config.offload_optimizer
+
+    def zero_offload_param(self):
+        return self._config.zero_config.offload_param
+
+    def fp16_enabled(self):
+        return self._config.fp16_enabled
+
+    def bfloat16_enabled(self):
+        return self._config.bfloat16_enabled
+
+    def amp_enabled(self):
+        return self._config.amp_enabled
+
+    def gradient_clipping(self):
+        return self._config.gradient_clipping
+
+    def wall_clock_breakdown(self):
+        return self._config.wall_clock_breakdown
+
+    def memory_breakdown(self):
+        return self._config.memory_breakdown
+
+    def get_lr(self):
+        return [g["lr"] for g in self.optimizer.param_groups] if self.optimizer else []
+
+    def get_mom(self):
+        return [g.get("betas", (g.get("momentum", 0), ))[0] for g in self.optimizer.param_groups]
+
+    def get_global_grad_norm(self):
+        return self.optimizer.get_global_grad_norm() if self.optimizer else None
+
+    @property
+    def loss_scale(self):
+        return self.optimizer.loss_scale if self.optimizer else 1.0
+
+    def get_data_parallel_group(self):
+        return self.seq_data_parallel_group
+
+    def is_gradient_accumulation_boundary(self):
+        if self._is_gradient_accumulation_boundary is None:
+            return (self.micro_steps + 1) % self.gradient_accumulation_steps() == 0
+        return self._is_gradient_accumulation_boundary
+
+    def set_gradient_accumulation_boundary(self, is_boundary):
+        self._is_gradient_accumulation_boundary = is_boundary
+
+    # ============================================================================================ data
+    def deepspeed_io(self, dataset, batch_size=None, route=None, pin_memory=True, data_sampler=None, collate_fn=None,
+                     num_local_io_workers=None):
+        return DeepSpeedDataLoader(dataset, batch_size or self.train_micro_batch_size_per_gpu(),
+                                   pin_memory and self.device.type == "cuda", self.local_rank, self.tput_timer,
+                                   collate_fn=collate_fn or self.collate_fn,
+                                   num_local_io_workers=num_local_io_workers, data_sampler=data_sampler,
+                                   data_parallel_world_size=self.dp_world_size,
+                                   data_parallel_rank=groups._get_data_parallel_rank(),
+                                   dataloader_drop_last=self._config.dataloader_drop_last)
+
+    # ============================================================================================ train loop
+    def train(self, mode=True):
+        self.module.train(mode)
+        return self
+
+    def eval(self):
+        self.module.eval()
+        return self
+
+    def forward(self, *inputs, **kwargs):
+        if self.flops_profiler is not None and self.global_steps == self._config.flops_profiler_config.profile_step \
+                and self.is_gradient_accumulation_boundary():
+            self.flops_profiler.start_profile(ignore_list=None)
+        self.timers(FORWARD_MICRO_TIMER).start()
+        if self.training and self.optimizer is not None:
+            self.optimizer.is_gradient_accumulation_boundary = self.is_gradient_accumulation_boundary()
+        loss = self.module(*inputs, **kwargs)
+        self.timers(FORWARD_MICRO_TIMER).stop()
+        return loss
+
+    def _scale_loss_by_gas(self, loss):
+        gas = self.gradient_accumulation_steps()
+        if gas > 1:
+            if torch.is_tensor(loss):
+                return loss / gas
+            if isinstance(loss, (list, tuple)):
+                return type(loss)(l / gas for l in loss)
+        return loss
+
+    def backward(self, loss, allreduce_gradients=True, release_loss=False, retain_graph=False, scale_wrt_gas=True):
+        assert self.optimizer is not None, "must provide an optimizer to call backward()"
+        self.timers(BACKWARD_MICRO_TIMER).start()
+        if scale_wrt_gas:
+            loss = self._scale_loss_by_gas(loss)
+        if self.monitor is not None and self.monitor.enabled and self.global_rank == 0 and \
+                self.is_gradient_accumulation_boundary():
+            self.monitor.write_events([("Train/Samples/train_loss", float(loss.detach()) *
+                                        self.gradient_accumulation_steps(), self.global_samples)])
+        self.optimizer.is_gradient_accumulation_boundary = self.is_gradient_accumulation_boundary()
+        self.optimizer.backward(loss, retain_graph=retain_graph)
+        self.timers(BACKWARD_MICRO_TIMER).stop()
+        return loss
+
+    def allreduce_gradients(self, bucket_size=None):
+        """Kept for API parity: reduction already happened in `backward` (bucketed on the comm stream)."""
+        return
+
+    def zero_grad(self):
+        self.module.zero_grad(set_to_none=False)
+
+    def step(self, lr_kwargs=None):
+        self.timers(STEP_MICRO_TIMER).start()
+        if self.is_gradient_accumulation_boundary():
+            if self.optimizer is not None:
+                self.optimizer.step()
+                overflow = self.optimizer.overflow
+                if overflow:
+                    self.skipped_steps += 1
+                elif self.lr_scheduler is not None:
+                    self.lr_scheduler.step(**(lr_kwargs or {}))
+                if self.optimizer.coordinator is not None:
+                    self.optimizer.coordinator.reset_step()
+            self.global_steps += 1
+            self.global_samples += self.train_batch_size()
+            if self.flops_profiler is not None and self.flops_profiler.started:
+                self.flops_profiler.stop_profile()
+                self.flops_profiler.print_model_profile(profile_step=self.global_steps)
+                self.flops_profiler.end_profile()
+            if self.monitor is not None and self.monitor.enabled and self.global_rank == 0:
+                ev = [("Train/Samples/lr", self.get_lr()[0], self.global_samples)]
+                if self.fp16_enabled():
+                    ev.append(("Train/Samples/loss_scale", self.optimizer.loss_scale, self.global_samples))
+                self.monitor.write_events(ev)
+            if self.global_steps % self.steps_per_print() == 0 and self.global_rank == 0:
+                log_dist(f"step={self.global_steps}, skipped={self.skipped_steps}, lr={self.get_lr()}", ranks=[0])
+        self.micro_steps += 1
+        self.timers(STEP_MICRO_TIMER).stop()
+
+    # ============================================================================================ checkpoints
+    def _get_ckpt_name(self, checkpoints_path, tag, mp_placeholder=None):
+        mp_rank = 0 if self.mpu is None else self.mpu.get_model_parallel_rank()
+        mp_str = mp_placeholder if mp_placeholder is not None else f"{mp_rank:02d}"
+        if self.zero_optimization_partition_weights():
+            dp_rank = dist.get_rank(self.seq_data_parallel_group)
+            return os.path.join(checkpoints_path, str(tag), f"{CK.ZERO_FILE_PREFIX}{dp_rank}_mp_rank_{mp_str}"
+                                f"{CK.MODEL_FILE_SUFFIX}")
+        return os.path.join(checkpoints_path, str(tag), f"{CK.MODEL_FILE_PREFIX}{mp_str}{CK.MODEL_FILE_SUFFIX}")
+
+    def _get_zero_ckpt_name(self, checkpoints_path, tag):
+        mp_rank = 0 if self.mpu is None else self.mpu.get_model_parallel_rank()
+        dp_rank = dist.get_rank(self.seq_data_parallel_group)
+        prefix = CK.BF16_ZERO_FILE_PREFIX if self.bfloat16_enabled() else CK.ZERO_FILE_PREFIX
+        return os.path.join(checkpoints_path, str(tag), f"{prefix}{dp_rank}_mp_rank_{mp_rank:02d}{CK.OPTIM_FILE_SUFFIX}")
+
+    def module_state_dict(self, destination=None, prefix="", keep_vars=False, exclude_frozen_parameters=False):
+        """Full module state dict; under ZeRO-3 (dp>1) this gathers every group (16-bit weights)."""
+        from .zero.partition_parameters import GatheredParameters
+        if self.zero_optimization_partition_weights() and self.dp_world_size > 1:
+            with GatheredParameters(list(self.module.parameters())):
+                sd = {k: v.detach().clone() for k, v in self.module.state_dict().items()}
+            return sd
+        return self.module.state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)
+
+    def _param_shapes(self):
+        shapes = OrderedDict()
+        for n, p in self.module.named_parameters():
+            if p.requires_grad:
+                shapes[n] = torch.Size(getattr(p, "ds_shape", p.shape))
+        return [shapes]
+
+    def _checkpoint_tag_validation(self, tag):
+        if not self._config.checkpoint_tag_validation_enabled or dist.get_world_size() == 1:
+            return
+        import hashlib
+        b = hashlib.sha1(str(tag).encode()).digest()
+        t = torch.tensor(list(b), dtype=torch.long, device=self.device)
+        mx, mn = t.clone(), t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        ok = bool(torch.equal(mx, mn))
+        if not ok:
+            msg = f"[rank={dist.get_rank()}] The checkpoint tag name '{tag}' is not consistent across all ranks"
+            if self._config.checkpoint_tag_validation_fail:
+                raise ValueError(msg)
+            logger.warning(msg)
+
+    def save_checkpoint(self, save_dir, tag=None, client_state={}, save_latest=True, exclude_frozen_parameters=False):
+        if tag is None:
+            tag = f"global_step{self.global_steps}"
+        tag = str(tag)
+        self._checkpoint_tag_validation(tag)
+        if dist.get_rank() == 0:
+            os.makedirs(os.path.join(save_dir, tag), exist_ok=True)
+        dist.barrier()
+        os.makedirs(os.path.join(save_dir, tag), exist_ok=True)
+        module_sd = self.module_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
+        zero = self.optimizer is not None
+        state = dict(module=module_sd if (self.save_non_zero_checkpoint or self.zero_optimization_stage() == 3)
+                     else None,
+                     buffer_names=[n for n, _ in self.module.named_buffers()],
+                     optimizer=None,
+                     param_shapes=self._param_shapes() if zero else None,
+                     frozen_param_shapes=None,
+                     shared_params=None,
+                     frozen_param_fragments=None,
+                     lr_scheduler=self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,
+                     data_sampler=None,
+                     random_ltd=None,
+                     sparse_tensor_module_names=list(self.sparse_tensor_module_names),
+                     skipped_steps=self.skipped_steps,
+                     global_steps=self.global_steps,
+                     global_samples=self.global_samples,
+                     dp_world_size=self.seq_dp_world_size,
+                     mp_world_size=self.mp_world_size,
+                     ds_config=self._config.param_dict,
+                     ds_version=_version())
+        state.update(client_state)
+        if self.save_non_zero_checkpoint:
+            self.checkpoint_engine.save(state, self._get_ckpt_name(save_dir, tag))
+        if zero:
+            osd = self.optimizer.state_dict()
+            zsd = dict(optimizer_state_dict=osd, ds_config=self._config.param_dict, ds_version=_version())
+            self.checkpoint_engine.save(zsd, self._get_zero_ckpt_name(save_dir, tag))
+            if dist.get_rank() == 0:
+                self._copy_recovery_script(save_dir)
+        self.checkpoint_engine.commit(tag)
+        dist.barrier()
+        if save_latest and dist.get_rank() == 0:
+            with open(os.path.join(save_dir, "latest"), "w") as f:
+                f.write(tag)
+        dist.barrier()
+        return True
+
+    def _copy_recovery_script(self, save_path):
+        import shutil
+        src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "utils", "zero_to_fp32.py")
+        if os.path.exists(src):
+            shutil.copyfile(src, os.path.join(save_path, "zero_to_fp32.py"))
+
+    def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
+                        load_lr_scheduler_states=True, load_module_only=False, custom_load_fn=None):
+        if tag is None:
+            latest = os.path.join(load_dir, "latest")
+            if not os.path.isfile(latest):
+                logger.warning(f"Unable to find latest file at {latest}")
+                return None, None
+            with open(latest) as f:
+                tag = f.read().strip()
+        path = self._get_ckpt_name(load_dir, tag)
+        if not os.path.exists(path) and self.zero_optimization_partition_weights():
+            # elastic: fewer files than ranks, read rank 0's module file (holds the full 16-bit module)
+            path = os.path.join(load_dir, str(tag), f"{CK.ZERO_FILE_PREFIX}0_mp_rank_00{CK.MODEL_FILE_SUFFIX}")
+        ck = self.checkpoint_engine.load(path, map_location="cpu")
+        self._load_module_state(ck["module"], strict=load_module_strict)
+        if not load_module_only and self.optimizer is not None:
+            zpath = self._get_zero_ckpt_name(load_dir, tag)
+            if os.path.exists(zpath):
+                zsd = self.checkpoint_engine.load(zpath, map_location="cpu")
+                osd = zsd["optimizer_state_dict"]
+                same_topology = osd.get(CK.PARTITION_COUNT, 1) == (self.optimizer.dp if self.optimizer.partition
+                                                                   else 1)
+                if same_topology:
+                    self.optimizer.load_state_dict(osd, load_optimizer_states=load_optimizer_states)
+                else:
+                    log_dist("DP world size changed since save: restoring fp32 masters from 16-bit weights "
+                             "(elastic load; optimizer moments reset)", ranks=[0])
+                    self.optimizer.refresh_from_module()
+            else:
+                self.optimizer.refresh_from_module()
+        if load_lr_scheduler_states and self.lr_scheduler is not None and ck.get("lr_scheduler") is not None:
+            self.lr_scheduler.load_state_dict(ck["lr_scheduler"])
+        self.global_steps = ck.get("global_steps", 0)
+        self.global_samples = ck.get("global_samples", self.global_steps * self.train_batch_size())
+        self.skipped_steps = ck.get("skipped_steps", 0)
+        client_state = {k: v for k, v in ck.items() if k not in _CKPT_KEYS}
+        return os.path.join(load_dir, str(tag)), client_state
+
+    @torch.no_grad()
+    def _load_module_state(self, sd, strict=True):
+        if self.zero_optimization_partition_weights() and self.optimizer is not None:
+            own = dict(self.module.named_parameters())
+            for n, v in sd.items():
+                if n in own:
+                    self.optimizer.set_full_fp32_param(own[n], v.to(self.device))
+            bufs = dict(self.module.named_buffers())
+            for n, v in sd.items():
+                if n in bufs:
+                    bufs[n].copy_(v)
+            return
+        self.module.load_state_dict(sd, strict=strict)
+        if self.optimizer is not None:
+            self.optimizer.refresh_from_module()
+
+    def save_16bit_model(self, save_dir, save_filename="pytorch_model.bin", exclude_frozen_parameters=False):
+        sd = self.module_state_dict()
+        if dist.get_rank() == 0:
+            os.makedirs(save_dir, exist_ok=True)
+            torch.save(sd, os.path.join(save_dir, save_filename))
+        dist.barrier()
+        return True
+
+    save_fp16_model = save_16bit_model
+
+
+_CKPT_KEYS = {
+    "module", "buffer_names", "optimizer", "param_shapes", "frozen_param_shapes", "shared_params",
+    "frozen_param_fragments", "lr_scheduler", "data_sampler", "random_ltd", "sparse_tensor_module_names",
+    "skipped_steps", "global_steps", "global_samples", "dp_world_size", "mp_world_size", "ds_config", "ds_version"
+}

@@ -1,0 +1,155 @@
+"""ZeRO-3 parameter fetch / release / prefetch (reference `runtime/zero/partitioned_param_coordinator.py:58-526`
+and the module hooks of `parameter_offload.py:342-540`).
+
+Per fetch group (one module's params in one flat buffer):
+  forward pre-hook  -> fetch (wait for an in-flight prefetch or gather now), then prefetch ahead along the trace
+  forward hook      -> release (unless we are inside a backward recompute)
+  backward pre-hook -> fetch again (params for the module's backward)
+  all grads ready   -> release (from the optimizer's grad hook)
+The trace of group fetches is recorded on the first step and replayed: at trace position i the coordinator issues
+`all_gather_into_tensor` on the dedicated `ag_stream` for the next groups up to `prefetch_bucket_size` elements,
+so xGMI transfers run under the current layer's GEMMs. A divergent fetch order invalidates the trace (re-record).
+"""
+import torch
+
+from ... import comm as dist
+from ...utils.logging import logger
+from .flat_optimizer import ZeroParamStatus
+from .linear import install_zero3_linear
+
+RECORD, COMPLETE, INVALID = 0, 1, 2
+
+
+class ParamCoordinator:
+
+    def __init__(self, opt, prefetch_bucket_size=int(5e7), max_live_parameters=int(1e9)):
+        self.opt = opt
+        self.prefetch_bucket_size = int(prefetch_bucket_size)
+        self.max_live = int(max_live_parameters)
+        self.trace = []
+        self.mode = RECORD
+        self.pos = 0
+        self.in_backward = False
+        self.ag_stream = opt.ag_stream
+        self.acc = opt.acc
+        self._hooks = []
+        self.live_numel = 0
+        install_zero3_linear(opt.module)
+        for g in opt.groups:
+            if g.persistent or g.module is None:
+                continue
+            m = g.module
+            m._ds_fetch_group = g
+            self._hooks.append(m.register_forward_pre_hook(self._pre_fwd))
+            self._hooks.append(m.register_forward_hook(self._post_fwd))
+            self._hooks.append(m.register_full_backward_pre_hook(self._pre_bwd))
+
+    # ----------------------------------------------------------------------------------- hooks
+    def _pre_fwd(self, m, inputs):
+        self.fetch(m._ds_fetch_group)
+
+    def _post_fwd(self, m, inputs, outputs):
+        if self.in_backward or torch._C._current_graph_task_id() != -1:
+            return  # activation-checkpoint recompute inside backward: keep params for the module's backward
+        self.release(m._ds_fetch_group)
+
+    def _pre_bwd(self, m, grad_output):
+        self.fetch(m._ds_fetch_group)
+
+    # ----------------------------------------------------------------------------------- core
+    def _issue(self, g):
+        opt = self.opt
+        if g.status != ZeroParamStatus.NOT_AVAILABLE:
+            return
+        compute = self.acc.current_stream() if self.ag_stream is not None else None
+        if self.ag_stream is not None:
+            self.ag_stream.wait_stream(compute)
+            with self.acc.stream(self.ag_stream):
+                g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
+                dist.all_gather_into_tensor(g.full, g.shard, group=opt.dp_group)
+                g.ag_event = self.acc.Event()
+                g.ag_event.record(self.ag_stream)
+        else:
+            g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
+            dist.all_gather_into_tensor(g.full, g.shard, group=opt.dp_group)
+            g.ag_event = None
+        g.status = ZeroParamStatus.INFLIGHT
+        self.live_numel += g.padded
+
+    def _wait(self, g):
+        if g.status == ZeroParamStatus.INFLIGHT:
+            if g.ag_event is not None:
+                cur = self.acc.current_stream()
+                cur.wait_event(g.ag_event)
+                g.full.record_stream(cur)
+            self.opt._point_params(g)
+            g.status = ZeroParamStatus.AVAILABLE
+
+    def fetch(self, g):
+        self._trace(g)
+        if g.status == ZeroParamStatus.NOT_AVAILABLE:
+            self._issue(g)
+        self._wait(g)
+        self._prefetch()
+
+    def release(self, g):
+        if g.persistent or g.status == ZeroParamStatus.NOT_AVAILABLE:
+            return
+        if g.status == ZeroParamStatus.INFLIGHT:
+            self._wait(g)
+        self.opt._release_params(g)
+        g.full = None
+        self.live_numel -= g.padded
+
+    def release_after_backward(self, g):
+        self.release(g)
+
+    # ----------------------------------------------------------------------------------- trace / prefetch
+    def _trace(self, g):
+        if self.mode == RECORD:
+            self.trace.append(g.idx)
+            return
+        if self.mode == COMPLETE:
+            if self.pos < len(self.trace) and self.trace[self.pos] == g.idx:
+                self.pos += 1
+            else:
+                logger.debug("ZeRO-3 fetch order diverged from the recorded trace; re-recording")
+                self.mode = INVALID
+
+    def _prefetch(self):
+        if self.mode != COMPLETE or self.prefetch_bucket_size <= 0:
+            return
+        budget = self.prefetch_bucket_size
+        i = self.pos
+        groups = self.opt.groups
+        while i < len(self.trace) and budget > 0:
+            g = groups[self.trace[i]]
+            if g.status == ZeroParamStatus.NOT_AVAILABLE:
+                if self.live_numel + g.padded > self.max_live:
+                    break
+                self._issue(g)
+            budget -= g.numel
+            i += 1
+
+    def begin_backward(self):
+        self.in_backward = True
+
+    def end_backward(self):
+        self.in_backward = False
+
+    def reset_step(self):
+        """End of an optimizer step: close the trace, release anything still gathered."""
+        if self.mode == RECORD:
+            self.mode = COMPLETE if self.trace else RECORD
+        elif self.mode == INVALID:
+            self.trace = []
+            self.mode = RECORD
+        self.pos = 0
+        for g in self.opt.groups:
+            if not g.persistent and g.status != ZeroParamStatus.NOT_AVAILABLE:
+                self.release(g)
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -1,0 +1,800 @@
+"""Flat-group ZeRO engine: one implementation for "no ZeRO" (bf16/fp16/fp32 DP), ZeRO-1, ZeRO-2 and ZeRO-3.
+
+Reference behaviour being reproduced: `runtime/zero/stage_1_and_2.py` (DeepSpeedZeroOptimizer: flatten, partition,
+IPG buckets, reduce, all-gather after step), `runtime/zero/stage3.py` (DeepSpeedZeroOptimizer_Stage3: param shards,
+reduce-scatter of grad buckets, sub-group stepping, Twin-Flow), `runtime/bf16_optimizer.py`,
+`runtime/fp16/fused_optimizer.py`.
+
+MI355X-first design (why it is not a port):
+* A FLAT GROUP is a set of parameters laid out back-to-back in ONE buffer of `seg * dp` elements. Rank r owns the
+  contiguous segment [r*seg, (r+1)*seg). Parameters are *views* into the gathered buffer, so
+  - ZeRO-3 fetch = one `all_gather_into_tensor(full, shard)` and zero copies (the reference gathers per-param shards
+    and unflattens with copies), released by swapping `p.data` back to an empty tensor;
+  - gradient reduction = one `reduce_scatter_tensor(seg_out, grad_flat)` straight into the owner's segment
+    (no interleave/pad copies as in the reference's `reduce_scatter_coalesced`);
+  - ZeRO-1/2 post-step refresh = one in-place `all_gather_into_tensor` per group.
+  With 288 GB of HBM per GPU the groups are big (per-module for ZeRO-3, `reduce_bucket_size` buckets otherwise),
+  so every collective is a large xGMI transfer instead of many small ones.
+* The optimizer works on per-optimizer-group fp32 master buffers made of "runs" (the intersection of a rank segment
+  with one optimizer param group). The gfx950 fused Adam kernel updates master + moments and writes the bf16/fp16
+  shard in the same pass (no separate cast), driven through the multi-tensor pointer table.
+* Reduction runs on dedicated HIP streams (`rs_stream` for reduce-scatter / all-reduce, `ag_stream` for ZeRO-3
+  prefetch all-gathers) and overlaps backward / forward compute; events order the hand-offs.
+* ZeRO-Offload / Offload++ Twin-Flow: the first `ratio` fraction of each optimizer group's runs keep master and
+  moments in pinned host memory and are stepped by the native CPU Adam CONCURRENTLY with the GPU part (the reference
+  runs CPU and GPU sub-groups sequentially, `stage3.py:1976-1992`); D2H of grads and H2D of the bf16 result use
+  non-blocking copies on a side stream.
+"""
+import math
+import os
+from collections import OrderedDict, defaultdict
+
+import torch
+import torch.nn as nn
+
+from ... import comm as dist
+from ...accelerator import get_accelerator
+from ...checkpoint import constants as CK
+from ...ops import native
+from ...ops.adam.fused_adam import FusedAdam
+from ...utils.logging import log_dist, logger
+from ..fp16.loss_scaler import CreateLossScaler
+from .config import ZeroStageEnum
+
+ALIGN = 64  # elements: keeps every rank segment 128-B (bf16) aligned for 16-B vector access
+
+
+def _ceil(a, b):
+    return (a + b - 1) // b
+
+
+def _pnumel(p):
+    """Logical numel (zero.Init-partitioned params have empty .data and carry ds_numel)."""
+    return p.ds_numel if hasattr(p, "ds_tensor") else p.numel()
+
+
+class ZeroParamStatus:
+    AVAILABLE = 1
+    NOT_AVAILABLE = 2
+    INFLIGHT = 3
+
+
+class FlatGroup:
+    """A set of parameters sharing one flat buffer and one collective."""
+
+    def __init__(self, idx, params, dp, rank, partition, persistent, device, dtype, module=None):
+        self.idx = idx
+        self.params = list(params)
+        self.module = module
+        self.dtype = dtype
+        self.device = device
+        self.offsets, self.numels = [], []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            self.numels.append(_pnumel(p))
+            off += _ceil(_pnumel(p), 8) * 8  # 16-B align each param view inside the buffer
+        self.numel = off
+        self.dp = dp if partition else 1
+        self.rank = rank if partition else 0
+        self.partition = partition
+        self.seg = _ceil(max(self.numel, 1), self.dp * ALIGN) * ALIGN if partition else _ceil(max(self.numel, 1), ALIGN) * ALIGN
+        self.padded = self.seg * self.dp
+        self.persistent = persistent
+        self.full = None          # gathered [padded] buffer (or None when released)
+        self.shard = None         # [seg] owner shard (view of full for persistent groups)
+        self.status = ZeroParamStatus.NOT_AVAILABLE
+        self.ag_work = None
+        self.ag_event = None
+        self.grad_flat = None
+        self.pending = 0
+        self.reduced_this_pass = False
+        self.runs = []            # (seg_lo, seg_hi, opt_group_idx, master_off, on_host)
+        self.trace_pos = []
+
+    @property
+    def seg_lo(self):
+        return self.rank * self.seg
+
+    def param_seg_ranges(self, gidx_of_param):
+        """Intersections of this rank's segment with each param: [(p_index, lo, hi)] in buffer coordinates."""
+        lo, hi = self.seg_lo, self.seg_lo + self.seg
+        out = []
+        for i, p in enumerate(self.params):
+            a, b = self.offsets[i], self.offsets[i] + self.numels[i]
+            s, e = max(a, lo), min(b, hi)
+            if s < e:
+                out.append((i, s, e))
+        return out
+
+
+class FlatZeroOptimizer:
+    """ZeRO stage 0/1/2/3 over flat groups. See module docstring."""
+
+    def __init__(self, init_optimizer, module, ds_config, dp_group=None, stage=0, mpu=None, clip_grad=0.0,
+                 dtype=torch.bfloat16, communication_data_type=None, zero_config=None, timers=None,
+                 gradient_accumulation_steps=1, expert_params=None):
+        self.optimizer = init_optimizer
+        self.module = module
+        self.stage = int(stage)
+        self.zc = zero_config
+        self.cfg = ds_config
+        self.dtype = dtype
+        self.clip_grad = clip_grad
+        self.dp_group = dp_group
+        self.dp = dist.get_world_size(dp_group)
+        self.rank = dist.get_rank(dp_group)
+        self.mpu = mpu
+        self.timers = timers
+        self.acc = get_accelerator()
+        self.device = torch.device(self.acc.device_name(self.acc.current_device())) if self.acc.device_name() != "cpu" \
+            else torch.device("cpu")
+        self.partition = self.stage >= 1 and self.dp > 1
+        self.comm_dtype = communication_data_type or dtype
+        self.gas = gradient_accumulation_steps
+        self.is_gradient_accumulation_boundary = True
+        self.micro_step = 0
+        self.global_steps = 0
+        self.overflow = False
+        self._global_grad_norm = None
+        self.offload = False
+        self.offload_ratio = 0.0
+        if self.zc is not None and self.zc.offload_optimizer is not None and \
+                str(self.zc.offload_optimizer.device.value if hasattr(self.zc.offload_optimizer.device, "value") else self.zc.offload_optimizer.device) in ("cpu", "nvme"):
+            self.offload = True
+            self.offload_ratio = float(self.zc.offload_optimizer.ratio)
+            self.offload_pin = bool(self.zc.offload_optimizer.pin_memory)
+        # fp16 loss scaling
+        fp16 = dtype == torch.float16
+        self.loss_scaler = CreateLossScaler(dtype, getattr(ds_config, "loss_scale", 0) or 1.0,
+                                            fp16 and getattr(ds_config, "loss_scale", 0) == 0,
+                                            getattr(ds_config, "dynamic_loss_scale_args", None))
+        self.dynamic_loss_scale = self.loss_scaler.dynamic
+        # streams
+        self.rs_stream = self.acc.Stream() if self.device.type == "cuda" else None
+        self.ag_stream = self.acc.Stream() if self.device.type == "cuda" else None
+        self._fused_adam = isinstance(self.optimizer, FusedAdam) or getattr(self.optimizer, "_ds_flat_adam", False)
+        self._build_groups()
+        self._build_master()
+        self._install_grad_hooks()
+        self.coordinator = None
+        if self.stage == 3 and self.dp > 1:
+            from .coordinator import ParamCoordinator
+            self.coordinator = ParamCoordinator(self, prefetch_bucket_size=self.zc.prefetch_bucket_size,
+                                                max_live_parameters=self.zc.max_live_parameters)
+        log_dist(f"FlatZeroOptimizer: stage={self.stage} dp={self.dp} groups={len(self.groups)} "
+                 f"params={sum(g.numel for g in self.groups) / 1e6:.1f}M partition={self.partition} "
+                 f"offload={self.offload}(ratio={self.offload_ratio}) fused_adam={self._fused_adam}", ranks=[0])
+
+    # ================================================================================ construction
+    def _trainable_params_in_order(self):
+        seen = set()
+        out = []
+        for og_idx, g in enumerate(self.optimizer.param_groups):
+            for p in g["params"]:
+                if p.requires_grad and id(p) not in seen:
+                    seen.add(id(p))
+                    out.append((p, og_idx))
+        return out
+
+    def _build_groups(self):
+        plist = self._trainable_params_in_order()
+        self.param_to_og = {id(p): og for p, og in plist}
+        self.opt_params = [p for p, _ in plist]
+        self.num_og = len(self.optimizer.param_groups)
+        groups = []
+        if self.stage == 3:
+            # one group per module that directly owns trainable params (fetch granularity = module), plus ONE
+            # persistent group for every small param (< param_persistence_threshold): never released.
+            thr = self.zc.param_persistence_threshold if self.dp > 1 else 0
+            owned = set()
+            persistent = []
+            for name, m in self.module.named_modules():
+                ps = [p for p in m.parameters(recurse=False) if id(p) in self.param_to_og and id(p) not in owned]
+                if not ps:
+                    continue
+                for p in ps:
+                    owned.add(id(p))
+                big = [p for p in ps if _pnumel(p) >= thr]
+                small = [p for p in ps if _pnumel(p) < thr]
+                persistent.extend(small)
+                if big:
+                    big.sort(key=lambda p: self.param_to_og[id(p)])
+                    groups.append(dict(params=big, persistent=self.dp == 1, module=m))
+            rest = [p for p in self.opt_params if id(p) not in owned]
+            persistent.extend(rest)
+            if persistent:
+                persistent.sort(key=lambda p: self.param_to_og[id(p)])
+                groups.append(dict(params=persistent, persistent=True, module=None))
+        else:
+            # buckets in REVERSE registration order (≈ backward order) so reduction of early buckets overlaps
+            # the rest of backward; bucket size from reduce_bucket_size (default 5e8 elements ≈ 1 GB bf16)
+            cap = int(self.zc.reduce_bucket_size) if self.zc is not None else int(5e8)
+            cur, cur_n = [], 0
+            for p in reversed(self.opt_params):
+                if cur and (cur_n + _pnumel(p) > cap or self.param_to_og[id(p)] != self.param_to_og[id(cur[-1])]):
+                    groups.append(dict(params=cur, persistent=True, module=None))
+                    cur, cur_n = [], 0
+                cur.append(p)
+                cur_n += _pnumel(p)
+            if cur:
+                groups.append(dict(params=cur, persistent=True, module=None))
+        self.groups = []
+        for i, d in enumerate(groups):
+            g = FlatGroup(i, d["params"], self.dp, self.rank, self.partition, d["persistent"], self.device,
+                          self.dtype, d["module"])
+            self.groups.append(g)
+        self.param_group = {}
+        for g in self.groups:
+            for i, p in enumerate(g.params):
+                self.param_group[id(p)] = (g, i)
+        self._materialize_buffers()
+
+    @torch.no_grad()
+    def _materialize_buffers(self):
+        """Move parameter data into flat buffers (full for persistent groups, shard-only for ZeRO-3)."""
+        for g in self.groups:
+            g._opt = self
+            full = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
+            for i, p in enumerate(g.params):
+                if getattr(p, "ds_tensor", None) is not None and p.data.numel() != p.ds_numel:
+                    # built under zero.Init: re-gather this one parameter and regroup it into the flat layout
+                    from .partition_parameters import gather_partitioned_param
+                    src = gather_partitioned_param(p)
+                else:
+                    src = p.data
+                full[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(src.reshape(-1))
+                if hasattr(p, "ds_tensor"):
+                    del p.ds_tensor
+            if g.persistent:
+                g.full = full
+                g.shard = full[g.seg_lo:g.seg_lo + g.seg]
+                self._point_params(g)
+                g.status = ZeroParamStatus.AVAILABLE
+            else:
+                g.shard = full[g.seg_lo:g.seg_lo + g.seg].clone()
+                del full
+                g.full = None
+                self._release_params(g)
+            for i, p in enumerate(g.params):
+                p.ds_numel = g.numels[i]
+                p.ds_persist = g.persistent
+                p.ds_group = g
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def _point_params(self, g):
+        for i, p in enumerate(g.params):
+            shape = getattr(p, "ds_shape", None) or p.shape
+            if not hasattr(p, "ds_shape"):
+                p.ds_shape = shape
+            p.data = g.full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(shape)
+            p.ds_status = ZeroParamStatus.AVAILABLE
+
+    def _release_params(self, g):
+        for i, p in enumerate(g.params):
+            if not hasattr(p, "ds_shape"):
+                p.ds_shape = p.shape
+            p.ds_numel = g.numels[i]
+            p.data = torch.empty(0, dtype=self.dtype, device=self.device)
+            p.ds_status = ZeroParamStatus.NOT_AVAILABLE
+        g.status = ZeroParamStatus.NOT_AVAILABLE
+
+    @torch.no_grad()
+    def _build_master(self):
+        """fp32 master / grad-accumulator buffers per optimizer group, as concatenated runs."""
+        og_len = [0] * self.num_og
+        run_specs = []
+        for g in self.groups:
+            ranges = g.param_seg_ranges(None)
+            # merge consecutive ranges of the same optimizer group (params are sorted by og within a group)
+            runs = []
+            for (i, s, e) in ranges:
+                og = self.param_to_og[id(g.params[i])]
+                if runs and runs[-1][2] == og and runs[-1][1] == s:
+                    runs[-1][1] = e
+                elif runs and runs[-1][2] == og:
+                    # gap = inter-param alignment padding: include it (it is zero and stays zero)
+                    runs[-1][1] = e
+                else:
+                    runs.append([s, e, og])
+            for s, e, og in runs:
+                run_specs.append((g, s, e, og))
+                og_len[og] += e - s
+        # Twin-Flow split: the first `ratio` of each og's elements live (and are stepped) on the host
+        host_budget = [int(l * self.offload_ratio) if self.offload else 0 for l in og_len]
+        self.master, self.master_host = [], []
+        self.grad_acc, self.grad_acc_host = [], []
+        dev_len = [0] * self.num_og
+        host_len = [0] * self.num_og
+        for g, s, e, og in run_specs:
+            n = e - s
+            on_host = host_len[og] + n <= host_budget[og] and self.offload
+            if on_host:
+                moff = host_len[og]
+                host_len[og] += n
+            else:
+                moff = dev_len[og]
+                dev_len[og] += n
+            g.runs.append((s - g.seg_lo, e - g.seg_lo, og, moff, on_host))
+        pin = self.device.type == "cuda" and self.offload and getattr(self, "offload_pin", True)
+        for og in range(self.num_og):
+            m = torch.zeros(dev_len[og], dtype=torch.float32, device=self.device)
+            self.master.append(m)
+            self.grad_acc.append(torch.zeros(dev_len[og], dtype=torch.float32, device=self.device))
+            hm = torch.zeros(host_len[og], dtype=torch.float32, pin_memory=pin) if host_len[og] else None
+            self.master_host.append(hm)
+            self.grad_acc_host.append(torch.zeros(host_len[og], dtype=torch.float32, pin_memory=pin)
+                                      if host_len[og] else None)
+        # fill master from the bf16 shards
+        for g in self.groups:
+            for (s, e, og, moff, on_host) in g.runs:
+                dst = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
+                dst.copy_(g.shard[s:e].float())
+        # hand the fp32 buffers to the wrapped optimizer (its param_groups / lr schedule stay authoritative)
+        self.fp32_flat = []
+        for og, group in enumerate(self.optimizer.param_groups):
+            mp = nn.Parameter(self.master[og], requires_grad=False)
+            mp.grad = self.grad_acc[og]
+            self.fp32_flat.append(mp)
+            group["params"] = [mp]
+        self.fp32_flat_host = []
+        for og in range(self.num_og):
+            if self.master_host[og] is not None:
+                hp = nn.Parameter(self.master_host[og], requires_grad=False)
+                hp.grad = self.grad_acc_host[og]
+                self.fp32_flat_host.append(hp)
+            else:
+                self.fp32_flat_host.append(None)
+        self.host_states = {}  # og -> (exp_avg, exp_avg_sq, step) for the Twin-Flow host part
+        self._grad_acc_valid = False
+
+    # ================================================================================ gradient path
+    def _preset_mode(self):
+        """Grad views into persistent flat buffers (accumulated by autograd in place) vs copy-into-bucket."""
+        return self.stage <= 1 or self.dp == 1
+
+    def _install_grad_hooks(self):
+        self._hooks = []
+        if self._preset_mode():
+            for g in self.groups:
+                g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
+                self._point_grads(g)
+        for p in self.opt_params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_ready_hook))
+
+    def _point_grads(self, g):
+        for i, p in enumerate(g.params):
+            p.grad = g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape)
+
+    def _begin_pass(self):
+        for g in self.groups:
+            g.pending = len(g.params)
+            g.reduced_this_pass = False
+
+    def _grad_ready_hook(self, p):
+        g, i = self.param_group[id(p)]
+        if self._preset_mode():
+            view = g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]]
+            if p.grad is None or p.grad.data_ptr() != view.data_ptr():
+                # someone reset p.grad (e.g. module.zero_grad(set_to_none=True)): fold it back into the flat buffer
+                if p.grad is not None:
+                    view.add_(p.grad.reshape(-1))
+                p.grad = view.view(p.ds_shape)
+        else:
+            if g.grad_flat is None:
+                g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
+            g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1))
+            p.grad = None
+        g.pending -= 1
+        if g.pending == 0 and self._should_reduce_now():
+            self._reduce_group(g)
+        if self.coordinator is not None and g.pending == 0 and not g.persistent:
+            self.coordinator.release_after_backward(g)
+
+    def _should_reduce_now(self):
+        # ZeRO-1 / no-ZeRO accumulate locally and reduce only at the accumulation boundary
+        return self.is_gradient_accumulation_boundary or self.stage >= 2
+
+    def _reduce_group(self, g):
+        if g.reduced_this_pass:
+            return
+        g.reduced_this_pass = True
+        src = g.grad_flat
+        compute = self.acc.current_stream() if self.rs_stream is not None else None
+        ctx = self.acc.stream(self.rs_stream) if self.rs_stream is not None else _nullctx()
+        if self.rs_stream is not None:
+            self.rs_stream.wait_stream(compute)
+        with ctx:
+            comm = src if src.dtype == self.comm_dtype else src.to(self.comm_dtype)
+            prescale = self.comm_dtype == torch.float16 and self.dp > 1
+            if prescale:
+                comm.mul_(1.0 / self.dp)
+            if self.dp == 1:
+                out = comm[:g.seg]
+            elif self.partition:
+                out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
+                dist.reduce_scatter_tensor(out, comm, group=self.dp_group)
+            else:
+                dist.all_reduce(comm, group=self.dp_group)
+                out = comm
+            alpha = 1.0 if (prescale or self.dp == 1) else 1.0 / self.dp
+            self._accumulate_runs(g, out, alpha)
+            if not self._preset_mode():
+                # bucket memory is dead after the collective; let the allocator reuse it once rs_stream is done
+                if self.rs_stream is not None:
+                    src.record_stream(self.rs_stream)
+                g.grad_flat = None
+
+    def _accumulate_runs(self, g, seg_grad, alpha):
+        first = not self._grad_acc_valid_for(g)
+        for (s, e, og, moff, on_host) in g.runs:
+            src = seg_grad[s:e]
+            if on_host:
+                dst = self.grad_acc_host[og][moff:moff + e - s]
+                tmp = src.float().mul_(alpha) if alpha != 1.0 else src.float()
+                if first:
+                    dst.copy_(tmp, non_blocking=True)
+                else:
+                    dst.add_(tmp.cpu())
+            else:
+                dst = self.grad_acc[og][moff:moff + e - s]
+                if first:
+                    torch.mul(src, alpha, out=dst) if alpha != 1.0 else dst.copy_(src)
+                else:
+                    dst.add_(src, alpha=alpha)
+        g._acc_valid = True
+
+    def _grad_acc_valid_for(self, g):
+        return getattr(g, "_acc_valid", False)
+
+    def backward_prologue(self):
+        self._begin_pass()
+        if self.coordinator is not None:
+            self.coordinator.begin_backward()
+
+    def backward(self, loss, retain_graph=False):
+        self.backward_prologue()
+        if self.dtype == torch.float16:
+            self.loss_scaler.backward(loss.float(), retain_graph=retain_graph)
+        else:
+            loss.backward(retain_graph=retain_graph)
+        self.backward_epilogue()
+
+    def backward_epilogue(self):
+        """Flush groups whose params got no grad this pass (unused params count as zero) and join streams."""
+        if self._should_reduce_now():
+            for g in self.groups:
+                if not g.reduced_this_pass:
+                    if g.grad_flat is None:
+                        g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
+                    self._reduce_group(g)
+        if self.rs_stream is not None:
+            self.acc.current_stream().wait_stream(self.rs_stream)
+        if self.coordinator is not None:
+            self.coordinator.end_backward()
+        self.micro_step += 1
+
+    # ================================================================================ step
+    def _unscale_factor(self):
+        return 1.0 / self.loss_scaler.loss_scale
+
+    @torch.no_grad()
+    def _global_norm_sq(self):
+        tensors = [t for t in self.grad_acc if t.numel() > 0]
+        if tensors and tensors[0].is_cuda:
+            sq = native.hip_ops().sumsq_multi(tensors)
+        else:
+            sq = sum((t.float().pow(2).sum() for t in tensors), torch.zeros((), device=self.device))
+        hs = [t for t in self.grad_acc_host if t is not None and t.numel() > 0]
+        if hs:
+            sq = sq + sum(t.pow(2).sum() for t in hs).to(sq.device)
+        if self.partition:
+            dist.all_reduce(sq, group=self.dp_group)
+        if self.mpu is not None and hasattr(self.mpu, "get_model_parallel_group") and \
+                self.mpu.get_model_parallel_world_size() > 1:
+            dist.all_reduce(sq, group=self.mpu.get_model_parallel_group())
+        return sq
+
+    @torch.no_grad()
+    def step(self, closure=None, lr_kwargs=None):
+        """Optimizer step at the accumulation boundary (the engine only calls it there)."""
+        scale = self._unscale_factor()
+        norm_sq = self._global_norm_sq()
+        norm = norm_sq.sqrt() * scale
+        # one device->host sync per step for overflow / clipping decisions
+        norm_f = float(norm)
+        self._global_grad_norm = norm_f
+        overflow = not math.isfinite(norm_f)
+        self.overflow = overflow
+        if self.dtype == torch.float16 or self.loss_scaler.dynamic:
+            self.loss_scaler.update_scale(overflow)
+        if overflow:
+            log_dist(f"Overflow detected. Skipping step. Attempted loss scale: {1 / scale}, reducing to "
+                     f"{self.loss_scaler.loss_scale}", ranks=[0])
+            self._zero_grad_buffers()
+            return
+        clip = 1.0
+        if self.clip_grad and self.clip_grad > 0 and norm_f > self.clip_grad:
+            clip = self.clip_grad / (norm_f + 1e-6)
+        grad_scale = scale * clip
+        host_thread = None
+        if self.offload and any(t is not None for t in self.master_host):
+            import threading
+            host_thread = threading.Thread(target=self._host_step, args=(grad_scale, ))
+            host_thread.start()
+        self._device_step(grad_scale)
+        if host_thread is not None:
+            host_thread.join()
+            self._host_writeback()
+        self._post_step_gather()
+        self._zero_grad_buffers()
+        self.global_steps += 1
+
+    def _device_step(self, grad_scale):
+        if self._fused_adam:
+            for og, group in enumerate(self.optimizer.param_groups):
+                fp = self.fp32_flat[og]
+                if fp.numel() == 0:
+                    continue
+                st = self.optimizer.state[fp]
+                if len(st) == 0:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(fp.data)
+                    st["exp_avg_sq"] = torch.zeros_like(fp.data)
+                st["step"] += 1
+                b1, b2 = group["betas"]
+                step = st["step"]
+                bc1 = 1 - b1**step if group.get("bias_correction", True) else 1.0
+                bc2 = 1 - b2**step if group.get("bias_correction", True) else 1.0
+                ps, ms, vs, gs, lps = [], [], [], [], []
+                for g in self.groups:
+                    for (s, e, og2, moff, on_host) in g.runs:
+                        if og2 != og or on_host:
+                            continue
+                        n = e - s
+                        ps.append(fp.data[moff:moff + n])
+                        ms.append(st["exp_avg"][moff:moff + n])
+                        vs.append(st["exp_avg_sq"][moff:moff + n])
+                        gs.append(self.grad_acc[og][moff:moff + n])
+                        lps.append(g.shard[s:e])
+                adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+                if fp.is_cuda:
+                    native.hip_ops().adam_multi(ps, ms, vs, gs, lps, group["lr"], b1, b2, group["eps"],
+                                                group["weight_decay"], bc1, bc2, grad_scale, adamw)
+                else:
+                    from ...ops import reference
+                    for p_, m_, v_, g_, lp_ in zip(ps, ms, vs, gs, lps):
+                        reference.adam_update(p_, m_, v_, g_, group["lr"], b1, b2, group["eps"],
+                                              group["weight_decay"], step, group.get("bias_correction", True), adamw,
+                                              grad_scale, lp_)
+        else:
+            # generic torch optimizer over the fp32 flats: unscale/clip grads in place, step, copy to shards
+            for og in range(self.num_og):
+                if grad_scale != 1.0:
+                    self.grad_acc[og].mul_(grad_scale)
+            self.optimizer.step()
+            for g in self.groups:
+                for (s, e, og, moff, on_host) in g.runs:
+                    if not on_host:
+                        g.shard[s:e].copy_(self.master[og][moff:moff + e - s])
+
+    def _host_step(self, grad_scale):
+        """Twin-Flow host half: native CPU Adam on pinned fp32 partitions (runs on a worker thread)."""
+        from ...ops.native import cpu_ops
+        torch.cuda.synchronize() if self.device.type == "cuda" else None
+        for og, group in enumerate(self.optimizer.param_groups):
+            hp = self.master_host[og]
+            if hp is None:
+                continue
+            st = self.host_states.get(og)
+            if st is None:
+                st = [torch.zeros_like(hp), torch.zeros_like(hp), 0]
+                self.host_states[og] = st
+            st[2] += 1
+            b1, b2 = group["betas"]
+            if not hasattr(self, "_host_lp"):
+                self._host_lp = {}
+            lp = self._host_lp.get(og)
+            if lp is None:
+                lp = torch.empty(hp.numel(), dtype=self.dtype, pin_memory=self.device.type == "cuda")
+                self._host_lp[og] = lp
+            cpu_ops().cpu_adam_update(hp, st[0], st[1], self.grad_acc_host[og], lp, st[2], group["lr"], b1, b2,
+                                      group["eps"], group["weight_decay"], group.get("bias_correction", True),
+                                      bool(getattr(self.optimizer, "adam_w_mode", True)), grad_scale)
+
+    def _host_writeback(self):
+        for g in self.groups:
+            for (s, e, og, moff, on_host) in g.runs:
+                if on_host:
+                    g.shard[s:e].copy_(self._host_lp[og][moff:moff + e - s], non_blocking=True)
+
+    def _post_step_gather(self):
+        """Refresh full params of persistent groups from the updated shards (ZeRO-1/2, ZeRO-3 persistent)."""
+        if not self.partition:
+            return
+        for g in self.groups:
+            if g.persistent and g.full is not None:
+                dist.all_gather_into_tensor(g.full, g.shard, group=self.dp_group)
+
+    def _zero_grad_buffers(self):
+        for g in self.groups:
+            g._acc_valid = False
+            if self._preset_mode() and g.grad_flat is not None:
+                g.grad_flat.zero_()
+        self.micro_step = 0
+
+    def zero_grad(self, set_to_none=True):
+        # grads live in the flat buffers; user-visible p.grad views are kept (preset mode) or None (copy mode)
+        pass
+
+    # ================================================================================ accessors / compat
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    @property
+    def loss_scale(self):
+        return self.loss_scaler.loss_scale
+
+    @property
+    def cur_scale(self):
+        return self.loss_scaler.loss_scale
+
+    def get_global_grad_norm(self):
+        return self._global_grad_norm
+
+    def scale_if_loss(self, loss):
+        return loss * self.loss_scaler.loss_scale if self.dtype == torch.float16 else loss
+
+    @torch.no_grad()
+    def get_full_fp32_param(self, p):
+        """Gather the fp32 master value of one parameter (reference `safe_get_full_fp32_param`)."""
+        g, i = self.param_group[id(p)]
+        seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
+        for (s, e, og, moff, on_host) in g.runs:
+            src = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
+            seg32[s:e].copy_(src)
+        if self.partition:
+            full = torch.empty(g.padded, dtype=torch.float32, device=self.device)
+            dist.all_gather_into_tensor(full, seg32, group=self.dp_group)
+        else:
+            full = seg32
+        return full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).clone()
+
+    @torch.no_grad()
+    def set_full_fp32_param(self, p, value):
+        g, i = self.param_group[id(p)]
+        flat = value.reshape(-1).to(torch.float32)
+        a = g.offsets[i]
+        for (s, e, og, moff, on_host) in g.runs:
+            lo, hi = g.seg_lo + s, g.seg_lo + e
+            x0, x1 = max(lo, a), min(hi, a + g.numels[i])
+            if x0 < x1:
+                dst = (self.master_host if on_host else self.master)[og]
+                dst[moff + x0 - lo:moff + x1 - lo].copy_(flat[x0 - a:x1 - a])
+                g.shard[x0 - g.seg_lo:x1 - g.seg_lo].copy_(flat[x0 - a:x1 - a])
+        if g.persistent and self.partition:
+            dist.all_gather_into_tensor(g.full, g.shard, group=self.dp_group)
+
+    @torch.no_grad()
+    def get_full_grad(self, p):
+        """Averaged fp32 gradient of one param (valid between backward at the boundary and step)."""
+        g, i = self.param_group[id(p)]
+        seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
+        for (s, e, og, moff, on_host) in g.runs:
+            src = (self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s]
+            seg32[s:e].copy_(src)
+        seg32.mul_(self._unscale_factor())
+        if self.partition:
+            full = torch.empty(g.padded, dtype=torch.float32, device=self.device)
+            dist.all_gather_into_tensor(full, seg32, group=self.dp_group)
+        else:
+            full = seg32
+        return full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).clone()
+
+    def layout(self):
+        """Describe the flat layout (for checkpoints / zero_to_fp32): per group: param names, shapes, offsets, seg."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        out = []
+        for g in self.groups:
+            out.append(dict(seg=g.seg, dp=g.dp, persistent=g.persistent,
+                            params=[(names.get(id(p), f"param_{id(p)}"), list(p.ds_shape), g.offsets[i], g.numels[i])
+                                    for i, p in enumerate(g.params)],
+                            runs=[(s, e, og, moff, on_host) for (s, e, og, moff, on_host) in g.runs]))
+        return out
+
+    # ================================================================================ checkpoint state
+    def state_dict(self):
+        sd = OrderedDict()
+        sd[CK.ZERO_STAGE] = self.stage
+        sd[CK.LOSS_SCALER] = self.loss_scaler
+        sd["dynamic_loss_scale"] = self.dynamic_loss_scale
+        sd["overflow"] = self.overflow
+        sd[CK.CLIP_GRAD] = self.clip_grad
+        sd[CK.PARTITION_COUNT] = self.dp if self.partition else 1
+        sd[CK.BASE_OPTIMIZER_STATE] = self.optimizer.state_dict()
+        sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS] = [m.detach().cpu() for m in self.master]
+        sd["fp32_host_partitions"] = [m.detach().clone() if m is not None else None for m in self.master_host]
+        sd["host_optimizer_states"] = {og: [s[0].clone(), s[1].clone(), s[2]] for og, s in self.host_states.items()}
+        sd[CK.FLAT_LAYOUT] = self.layout()
+        sd[CK.DS_VERSION] = _version()
+        return sd
+
+    @torch.no_grad()
+    def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
+        if load_optimizer_states:
+            base = sd[CK.BASE_OPTIMIZER_STATE]
+            # our fp32 flat params are the optimizer params; restore states tensor-by-tensor onto device
+            saved_groups = base["param_groups"]
+            for og, group in enumerate(self.optimizer.param_groups):
+                for k, v in saved_groups[og].items():
+                    if k != "params":
+                        group[k] = v
+            for og, fp in enumerate(self.fp32_flat):
+                key = base["param_groups"][og]["params"][0]
+                st = base["state"].get(key, {})
+                self.optimizer.state[fp] = {
+                    k: (v.to(self.device) if torch.is_tensor(v) and v.dim() > 0 else v)
+                    for k, v in st.items()
+                }
+            for og, s in sd.get("host_optimizer_states", {}).items():
+                self.host_states[int(og)] = [s[0].clone(), s[1].clone(), s[2]]
+        if CK.LOSS_SCALER in sd:
+            self.loss_scaler = sd[CK.LOSS_SCALER]
+        self.dynamic_loss_scale = sd.get("dynamic_loss_scale", self.dynamic_loss_scale)
+        self.overflow = sd.get("overflow", False)
+        if load_from_fp32_weights:
+            for og, m in enumerate(sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS]):
+                self.master[og].copy_(m.to(self.device))
+            for og, m in enumerate(sd.get("fp32_host_partitions", [])):
+                if m is not None and self.master_host[og] is not None:
+                    self.master_host[og].copy_(m)
+            # refresh low-precision shards from masters
+            for g in self.groups:
+                for (s, e, og, moff, on_host) in g.runs:
+                    src = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
+                    g.shard[s:e].copy_(src.to(g.shard.device))
+            self._post_step_gather()
+
+    def refresh_from_module(self):
+        """Re-read master weights from the (possibly externally modified) bf16 shards."""
+        for g in self.groups:
+            for (s, e, og, moff, on_host) in g.runs:
+                dst = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
+                dst.copy_(g.shard[s:e].float())
+
+
+class _nullctx:
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _version():
+    from ... import __version__
+    return __version__
+
+
+# Reference-named entry points -------------------------------------------------------------------------------
+class DeepSpeedZeroOptimizer(FlatZeroOptimizer):
+    """ZeRO stage 1/2 (reference `runtime/zero/stage_1_and_2.py:96`)."""
+
+
+class DeepSpeedZeroOptimizer_Stage3(FlatZeroOptimizer):
+    """ZeRO stage 3 (reference `runtime/zero/stage3.py:73`)."""
+
+
+class BF16_Optimizer(FlatZeroOptimizer):
+    """bf16 params + fp32 master without ZeRO partitioning (reference `runtime/bf16_optimizer.py:30`)."""
+
+
+class FP16_Optimizer(FlatZeroOptimizer):
+    """fp16 params + fp32 master + dynamic loss scale (reference `runtime/fp16/fused_optimizer.py:31`)."""

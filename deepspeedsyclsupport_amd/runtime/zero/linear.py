@@ -1,0 +1,51 @@
+"""Memory-efficient linear for ZeRO-3 (reference `runtime/zero/linear.py:43` LinearFunctionForZeroStage3).
+
+torch's `F.linear` saves `weight.t()` — a VIEW of the gathered buffer — for backward, which would keep every
+layer's gathered weights alive until backward and defeat partitioning. This autograd function saves the Parameter
+itself, so releasing (`p.data = empty`) frees the gathered buffer and the backward pre-hook's re-gather is what the
+backward matmuls read.
+"""
+import types
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class LinearFunctionForZeroStage3(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, weight, bias=None):
+        ctx.save_for_backward(x, weight, bias)
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, go):
+        x, weight, bias = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = go.matmul(weight)
+        if ctx.needs_input_grad[1]:
+            gw = go.reshape(-1, go.shape[-1]).t().matmul(x.reshape(-1, x.shape[-1]))
+        if bias is not None and ctx.needs_input_grad[2]:
+            gb = go.reshape(-1, go.shape[-1]).sum(0)
+        return gx, gw, gb
+
+
+def zero3_linear_wrap(input, weight, bias=None):
+    return LinearFunctionForZeroStage3.apply(input, weight, bias)
+
+
+def _zero3_linear_forward(self, x):
+    return LinearFunctionForZeroStage3.apply(x, self.weight, self.bias)
+
+
+def install_zero3_linear(module: nn.Module):
+    """Route every nn.Linear in `module` through LinearFunctionForZeroStage3 (idempotent)."""
+    n = 0
+    for m in module.modules():
+        if isinstance(m, nn.Linear) and not getattr(m, "_ds_zero3_linear", False):
+            m.forward = types.MethodType(_zero3_linear_forward, m)
+            m._ds_zero3_linear = True
+            n += 1
+    return n

@@ -1,0 +1,229 @@
+"""`zero.Init` (construct a model already partitioned) and `GatheredParameters` (temporarily materialise partitioned
+params), reference `runtime/zero/partition_parameters.py:303-2134`.
+
+Init: while active, every nn.Module's `__init__` is post-processed: its freshly created parameters are moved to the
+GPU, cast to the training dtype, made identical across ranks (broadcast from rank 0, as the reference does at
+`:423`) and reduced to this rank's 1/dp slice `p.ds_tensor`; `p.data` becomes empty. The model never exists in full
+on any GPU, so a 70B model can be built on a node whose per-GPU memory only holds its shard. `DeepSpeedEngine` then
+regroups these per-parameter shards into its flat groups one parameter at a time.
+"""
+import functools
+
+import torch
+import torch.nn as nn
+
+from ... import comm as dist
+from ...accelerator import get_accelerator
+from ...parallel import groups
+from .flat_optimizer import ZeroParamStatus
+
+_init_depth = 0
+
+
+def _ceil(a, b):
+    return (a + b - 1) // b
+
+
+def shutdown_init_context():
+    """Called by `initialize()` (reference `partition_parameters.py:shutdown_init_context`)."""
+    return None
+
+
+def restore_init_context():
+    return None
+
+
+def is_zero_param(p):
+    return hasattr(p, "ds_tensor") or hasattr(p, "ds_group")
+
+
+@torch.no_grad()
+def _partition_param(p, dp, rank, group, device, dtype):
+    if hasattr(p, "ds_tensor"):
+        return
+    data = p.data.to(device=device, dtype=dtype if p.is_floating_point() else p.dtype)
+    if dp > 1:
+        dist.broadcast(data, groups._get_broadcast_src_rank() if groups.mpu else 0, group=group)
+    n = data.numel()
+    per = _ceil(n, dp)
+    flat = torch.zeros(per * dp, dtype=data.dtype, device=device)
+    flat[:n].copy_(data.reshape(-1))
+    p.ds_tensor = flat[rank * per:(rank + 1) * per].clone()
+    p.ds_shape = data.shape
+    p.ds_numel = n
+    p.ds_status = ZeroParamStatus.NOT_AVAILABLE
+    p.ds_process_group = group
+    p.data = torch.empty(0, dtype=data.dtype, device=device)
+
+
+@torch.no_grad()
+def gather_partitioned_param(p):
+    """Full tensor of a `zero.Init`-partitioned param (not yet adopted by an engine)."""
+    group = getattr(p, "ds_process_group", None)
+    dp = dist.get_world_size(group)
+    full = torch.empty(p.ds_tensor.numel() * dp, dtype=p.ds_tensor.dtype, device=p.ds_tensor.device)
+    if dp > 1:
+        dist.all_gather_into_tensor(full, p.ds_tensor, group=group)
+    else:
+        full.copy_(p.ds_tensor)
+    return full[:p.ds_numel].view(p.ds_shape)
+
+
+class Init:
+    """Context manager: modules built inside are partitioned at construction (see module docstring)."""
+
+    def __init__(self, module=None, data_parallel_group=None, mem_efficient_linear=True, remote_device=None,
+                 pin_memory=False, config_dict_or_path=None, config=None, enabled=True, dtype=None, mpu=None,
+                 zero_param_parallel_group=None, zero_quantized_weights=False, zero_quantized_nontrainable_weights=False,
+                 sequence_data_parallel_group=None, param_swapper=None):
+        self.enabled = enabled
+        if not enabled:
+            return
+        if not dist.is_initialized():
+            dist.init_distributed()
+        self.group = sequence_data_parallel_group or data_parallel_group or groups._get_sequence_data_parallel_group()
+        self.dp = dist.get_world_size(self.group)
+        self.rank = dist.get_rank(self.group)
+        acc = get_accelerator()
+        self.device = torch.device("cuda", acc.current_device()) if acc.device_name() == "cuda" else \
+            torch.device("cpu")
+        if remote_device == "cpu":
+            self.device = torch.device("cpu")
+        if dtype is None:
+            cfg = config_dict_or_path or config
+            dtype = torch.float32
+            if isinstance(cfg, dict):
+                if cfg.get("bf16", {}).get("enabled"):
+                    dtype = torch.bfloat16
+                elif cfg.get("fp16", {}).get("enabled"):
+                    dtype = torch.float16
+        self.dtype = dtype
+        if module is not None:
+            self._convert(module)
+
+    def _convert(self, module):
+        for m in module.modules():
+            for p in m.parameters(recurse=False):
+                _partition_param(p, self.dp, self.rank, self.group, self.device, self.dtype)
+
+    def __enter__(self):
+        global _init_depth
+        if not self.enabled:
+            return self
+        _init_depth += 1
+        self._orig_init = nn.Module.__init__
+        ctx = self
+        orig = self._orig_init
+
+        # patch every Module subclass' __init__ through the base: convert params owned directly by the module
+        self._patched = {}
+
+        def _wrap(cls):
+            init = cls.__dict__.get("__init__")
+            if init is None or getattr(init, "_ds_wrapped", False):
+                return
+
+            @functools.wraps(init)
+            def wrapped(module, *a, **k):
+                init(module, *a, **k)
+                for p in module.parameters(recurse=False):
+                    _partition_param(p, ctx.dp, ctx.rank, ctx.group, ctx.device, ctx.dtype)
+
+            wrapped._ds_wrapped = True
+            self._patched[cls] = init
+            cls.__init__ = wrapped
+
+        def _all_subclasses(c):
+            out = set()
+            for s in c.__subclasses__():
+                out.add(s)
+                out |= _all_subclasses(s)
+            return out
+
+        for cls in _all_subclasses(nn.Module):
+            _wrap(cls)
+        self._wrap = _wrap
+        # classes defined inside the context get wrapped on subclass creation
+        self._had_init_subclass = "__init_subclass__" in nn.Module.__dict__
+        self._orig_init_subclass = nn.Module.__dict__.get("__init_subclass__")
+
+        def init_subclass(cls, **kw):
+            _wrap(cls)
+
+        nn.Module.__init_subclass__ = classmethod(init_subclass)
+        return self
+
+    def __exit__(self, *exc):
+        global _init_depth
+        if not self.enabled:
+            return False
+        for cls, init in self._patched.items():
+            cls.__init__ = init
+        if self._had_init_subclass:
+            nn.Module.__init_subclass__ = self._orig_init_subclass
+        else:
+            del nn.Module.__init_subclass__
+        _init_depth -= 1
+        return False
+
+
+class GatheredParameters:
+    """Materialise partitioned params inside the block; with `modifier_rank`, changes made on that rank are
+    broadcast and written back into every rank's shard and fp32 master on exit."""
+
+    def __init__(self, params, modifier_rank=None, fwd_module=None, enabled=True):
+        if isinstance(params, nn.Parameter) or torch.is_tensor(params):
+            params = [params]
+        self.params = [p for p in params if is_zero_param(p)]
+        self.modifier_rank = modifier_rank
+        self.enabled = enabled and len(self.params) > 0
+        self._gathered_groups = []
+        self._gathered_init = []
+
+    def __enter__(self):
+        if not self.enabled:
+            return self
+        seen = set()
+        for p in self.params:
+            g = getattr(p, "ds_group", None)
+            if g is not None:
+                if id(g) in seen:
+                    continue
+                seen.add(id(g))
+                if g.status != ZeroParamStatus.AVAILABLE:
+                    opt = g._opt
+                    full = torch.empty(g.padded, dtype=g.dtype, device=g.device)
+                    dist.all_gather_into_tensor(full, g.shard, group=opt.dp_group)
+                    g.full = full
+                    opt._point_params(g)
+                    g.status = ZeroParamStatus.AVAILABLE
+                    self._gathered_groups.append(g)
+            elif hasattr(p, "ds_tensor") and p.data.numel() != p.ds_numel:
+                p.data = gather_partitioned_param(p).clone()
+                self._gathered_init.append(p)
+        return self
+
+    def __exit__(self, *exc):
+        if not self.enabled:
+            return False
+        if self.modifier_rank is not None:
+            for p in self.params:
+                g = getattr(p, "ds_group", None)
+                grp = g._opt.dp_group if g is not None else getattr(p, "ds_process_group", None)
+                if dist.get_world_size(grp) > 1:
+                    dist.broadcast(p.data, dist.get_global_rank(grp, self.modifier_rank), group=grp)
+                if g is not None:
+                    g._opt.set_full_fp32_param(p, p.data)
+                elif hasattr(p, "ds_tensor"):
+                    dp = dist.get_world_size(getattr(p, "ds_process_group", None))
+                    r = dist.get_rank(getattr(p, "ds_process_group", None))
+                    per = p.ds_tensor.numel()
+                    flat = torch.zeros(per * dp, dtype=p.ds_tensor.dtype, device=p.ds_tensor.device)
+                    flat[:p.ds_numel].copy_(p.data.reshape(-1))
+                    p.ds_tensor.copy_(flat[r * per:(r + 1) * per])
+        for g in self._gathered_groups:
+            g._opt._release_params(g)
+            g.full = None
+        for p in self._gathered_init:
+            p.data = torch.empty(0, dtype=p.ds_tensor.dtype, device=p.ds_tensor.device)
+        return False

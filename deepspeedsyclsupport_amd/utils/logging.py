@@ -1,0 +1,47 @@
+"""Rank-aware logging (`deepspeed/utils/logging.py` parity: `logger`, `log_dist`, `print_json_dist`)."""
+import json
+import logging
+import os
+import sys
+
+import torch.distributed as dist
+
+_FMT = "[%(asctime)s] [%(levelname)s] [%(filename)s:%(lineno)d:%(funcName)s] %(message)s"
+
+
+def _create_logger(name="DeepSpeedAMD", level=logging.INFO):
+    lg = logging.getLogger(name)
+    lg.setLevel(level)
+    lg.propagate = False
+    if not lg.handlers:
+        h = logging.StreamHandler(stream=sys.stdout)
+        h.setFormatter(logging.Formatter(_FMT))
+        lg.addHandler(h)
+    return lg
+
+
+logger = _create_logger(level=getattr(logging, os.environ.get("DS_LOG_LEVEL", "INFO").upper(), logging.INFO))
+
+
+def _rank():
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def log_dist(message, ranks=None, level=logging.INFO):
+    """Log on the listed ranks only (None or [-1] means every rank)."""
+    my = _rank()
+    if ranks is None or -1 in ranks or my in ranks:
+        logger.log(level, f"[Rank {my}] {message}")
+
+
+def print_json_dist(message, ranks=None, path=None):
+    my = _rank()
+    if ranks is None or -1 in ranks or my in ranks:
+        message["rank"] = my
+        with open(path, "w") as f:
+            json.dump(message, f)
+            os.fsync(f)
+
+
+def should_log_le(max_log_level_str):
+    return logger.getEffectiveLevel() <= getattr(logging, max_log_level_str.upper())

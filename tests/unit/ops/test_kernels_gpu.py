@@ -1,0 +1,237 @@
+"""Numerics of every gfx950 kernel against a plain-PyTorch fp32 reference of the same op
+(tolerances as the reference's inference_test_utils: bf16 looser, fp32 tight)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deepspeedsyclsupport_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: dict(rtol=2e-5, atol=2e-5), torch.bfloat16: dict(rtol=2e-2, atol=2e-2),
+       torch.float16: dict(rtol=3e-3, atol=3e-3)}
+
+
+def ops():
+    from deepspeedsyclsupport_amd.ops.native import hip_ops
+    return hip_ops()
+
+
+@pytest.mark.parametrize("n", [1, 1000, 65536 + 3, 1 << 20])
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("adamw", [True, False])
+def test_adam_flat(n, gdt, adamw):
+    torch.manual_seed(0)
+    p = torch.randn(n, device="cuda")
+    m = torch.randn(n, device="cuda").abs() * 0.1
+    v = torch.rand(n, device="cuda") * 0.1
+    g = torch.randn(n, device="cuda").to(gdt)
+    lp = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    step, lr, b1, b2, eps, wd, gs = 3, 1e-2, 0.9, 0.95, 1e-8, 0.1, 0.5
+    ops().adam_flat(p, m, v, g, lp, lr, b1, b2, eps, wd, 1 - b1**step, 1 - b2**step, gs, adamw)
+    R.adam_update(pr, mr, vr, g, lr, b1, b2, eps, wd, step, True, adamw, gs)
+    torch.testing.assert_close(p, pr, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m, mr, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(v, vr, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(lp.float(), pr.bfloat16().float(), rtol=0, atol=0)
+
+
+def test_adam_flat_misaligned():
+    n = 4099
+    base = torch.randn(n + 1, device="cuda")
+    p = base[1:]  # 4-byte offset: forces the scalar path
+    m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    g = torch.randn(n, device="cuda")
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    ops().adam_flat(p, m, v, g, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1.0, True)
+    R.adam_update(pr, mr, vr, g, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1)
+    torch.testing.assert_close(p, pr, rtol=1e-5, atol=1e-6)
+
+
+def test_adam_multi_and_fused_adam_optimizer():
+    from deepspeedsyclsupport_amd.ops.adam import FusedAdam
+    torch.manual_seed(1)
+    shapes = [(3, 5), (1024, ), (257, 33), (64, 64)] * 10  # > 32 tensors: two launches
+    ps = [torch.nn.Parameter(torch.randn(s, device="cuda")) for s in shapes]
+    refs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FusedAdam(ps, lr=1e-2, weight_decay=0.01)
+    ropt = torch.optim.AdamW(refs, lr=1e-2, weight_decay=0.01, eps=1e-8)
+    for _ in range(3):
+        for p, r in zip(ps, refs):
+            g = torch.randn_like(p)
+            p.grad, r.grad = g, g.clone()
+        opt.step()
+        ropt.step()
+    for p, r in zip(ps, refs):
+        torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-6)
+
+
+def test_lion_adagrad_lamb():
+    torch.manual_seed(2)
+    n = 100003
+    p, m, g = torch.randn(n, device="cuda"), torch.randn(n, device="cuda") * .1, torch.randn(n, device="cuda")
+    pr, mr = p.clone(), m.clone()
+    ops().lion_flat(p, m, g, None, 1e-3, 0.9, 0.99, 0.1, 1.0)
+    R.lion_update(pr, mr, g, 1e-3, 0.9, 0.99, 0.1)
+    torch.testing.assert_close(p, pr)
+    torch.testing.assert_close(m, mr)
+    s = torch.rand(n, device="cuda")
+    sr, pr = s.clone(), p.clone()
+    ops().adagrad_flat(p, s, g, None, 1e-2, 1e-10, 0.01, 1.0)
+    R.adagrad_update(pr, sr, g, 1e-2, 1e-10, 0.01)
+    torch.testing.assert_close(p, pr)
+    v = torch.rand(n, device="cuda") * 0.01
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    c = ops().lamb_flat(p, m, v, g, None, 1e-3, 0.9, 0.999, 1e-6, 0.01, 0.1, 0.001, 1.0, 10.0, 0.01)
+    trust = R.lamb_update(pr, mr, vr, g, 1e-3, 0.9, 0.999, 1e-6, 0.01, 1, True, 1.0, 10.0, 0.01)
+    assert abs(float(c) - trust) < 1e-4 * max(1.0, trust)
+    torch.testing.assert_close(p, pr, rtol=1e-5, atol=1e-6)
+
+
+def test_sumsq_multi():
+    xs = [torch.randn(n, device="cuda", dtype=dt) for n, dt in [(1000, torch.float32), (77777, torch.bfloat16),
+                                                                 (5, torch.float32), (1 << 20, torch.bfloat16)]]
+    ref = sum(float(x.float().pow(2).sum()) for x in xs)
+    got = float(ops().sumsq_multi(xs))
+    assert abs(got - ref) / ref < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H", [64, 1024, 4096, 5120, 8192])
+@pytest.mark.parametrize("residual", [False, True])
+def test_rms_norm_fwd_bwd(dtype, H, residual):
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(3)
+    rows = 37
+    x = torch.randn(rows, H, device="cuda", dtype=dtype, requires_grad=True)
+    r = torch.randn(rows, H, device="cuda", dtype=dtype, requires_grad=True) if residual else None
+    w = (1 + 0.1 * torch.randn(H, device="cuda", dtype=dtype)).requires_grad_(True)
+    out = DF.rms_norm(x, w, 1e-5, r)
+    y = out[0] if residual else out
+    xf = x.detach().float().requires_grad_(True)
+    rf = r.detach().float().requires_grad_(True) if residual else None
+    wf = w.detach().float().requires_grad_(True)
+    h = xf + rf if residual else xf
+    yr = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    torch.testing.assert_close(y.float(), yr, **TOL[dtype])
+    gy = torch.randn_like(yr)
+    loss = (y.float() * gy).sum() + ((out[1].float() * gy).sum() if residual else 0)
+    loss.backward()
+    lr_ = (yr * gy).sum() + ((h * gy).sum() if residual else 0)
+    lr_.backward()
+    torch.testing.assert_close(x.grad.float(), xf.grad, **TOL[dtype])
+    tol = dict(rtol=5e-2, atol=5e-1) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(w.grad.float(), wf.grad, **tol)
+    if residual:
+        torch.testing.assert_close(r.grad.float(), rf.grad, **TOL[dtype])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H", [768, 1024, 4096])
+def test_layer_norm_fwd_bwd(dtype, H):
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(4)
+    x = torch.randn(33, H, device="cuda", dtype=dtype, requires_grad=True)
+    g = (1 + 0.1 * torch.randn(H, device="cuda", dtype=dtype)).requires_grad_(True)
+    b = (0.1 * torch.randn(H, device="cuda", dtype=dtype)).requires_grad_(True)
+    y = DF.layer_norm(x, g, b, 1e-5)
+    xf, gf, bf = [t.detach().float().requires_grad_(True) for t in (x, g, b)]
+    yr = F.layer_norm(xf, (H, ), gf, bf, 1e-5)
+    torch.testing.assert_close(y.float(), yr, **TOL[dtype])
+    gy = torch.randn_like(yr)
+    (y.float() * gy).sum().backward()
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xf.grad, **TOL[dtype])
+    tol = dict(rtol=5e-2, atol=5e-1) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(g.grad.float(), gf.grad, **tol)
+    torch.testing.assert_close(b.grad.float(), bf.grad, **tol)
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu", "gelu_tanh", "relu"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gated_act(act, dtype):
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(5)
+    gu = torch.randn(19, 2 * 1376, device="cuda", dtype=dtype, requires_grad=True)
+    y = DF.gated_activation(gu, act)
+    gf = gu.detach().float().requires_grad_(True)
+    a, u = gf.chunk(2, -1)
+    fn = {"silu": F.silu, "gelu": F.gelu, "gelu_tanh": lambda t: F.gelu(t, approximate="tanh"), "relu": F.relu}[act]
+    yr = fn(a) * u
+    torch.testing.assert_close(y.float(), yr, **TOL[dtype])
+    gy = torch.randn_like(yr)
+    (y.float() * gy).sum().backward()
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(gu.grad.float(), gf.grad, **TOL[dtype])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_bias_act(dtype):
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    x = torch.randn(13, 3072, device="cuda", dtype=dtype, requires_grad=True)
+    b = torch.randn(3072, device="cuda", dtype=dtype, requires_grad=True)
+    y = DF.bias_activation(x, b, "gelu_tanh")
+    xf, bf = x.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True)
+    yr = F.gelu(xf + bf, approximate="tanh")
+    torch.testing.assert_close(y.float(), yr, **TOL[dtype])
+    gy = torch.randn_like(yr)
+    (y.float() * gy).sum().backward()
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xf.grad, **TOL[dtype])
+
+
+@pytest.mark.parametrize("hq,hk", [(8, 8), (8, 2)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_qkv_rope_split(hq, hk, dtype):
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(6)
+    B, S, D = 2, 33, 128
+    cos, sin = R.rope_tables(128, D, device="cuda")
+    qkv = torch.randn(B, S, hq + 2 * hk, D, device="cuda", dtype=dtype, requires_grad=True)
+    q, k, v = DF.qkv_rope_split(qkv, cos, sin, hq, hk)
+    qf = qkv.detach().float().requires_grad_(True)
+    qq, kk, vv = qf.split([hq, hk, hk], dim=2)
+    pos = torch.arange(S, device="cuda")
+    qr = R.apply_rope_half(qq, cos, sin, pos).transpose(1, 2)
+    kr = R.apply_rope_half(kk, cos, sin, pos).transpose(1, 2)
+    vr = vv.transpose(1, 2)
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        torch.testing.assert_close(a.float(), b, **TOL[dtype])
+    gs = [torch.randn_like(t) for t in (qr, kr, vr)]
+    sum((a.float() * g).sum() for a, g in zip((q, k, v), gs)).backward()
+    sum((a * g).sum() for a, g in zip((qr, kr, vr), gs)).backward()
+    torch.testing.assert_close(qkv.grad.float(), qf.grad, **TOL[dtype])
+
+
+@pytest.mark.parametrize("interleaved", [False, True])
+def test_rope_inplace(interleaved):
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    B, S, H, D = 2, 17, 4, 64
+    cos, sin = R.rope_tables(64, D, device="cuda")
+    x = torch.randn(B, S, H, D, device="cuda")
+    ref = DF.apply_rotary_pos_emb(x.clone().cpu(), cos.cpu(), sin.cpu(), interleaved=interleaved)
+    got = DF.apply_rotary_pos_emb(x.clone(), cos, sin, interleaved=interleaved)
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-5, atol=1e-5)
+    back = DF.apply_rotary_pos_emb(got.clone(), cos, sin, interleaved=interleaved, inverse=True)
+    torch.testing.assert_close(back, x, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("V", [32000, 50257, 1000])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cross_entropy(V, dtype):
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(7)
+    N = 67
+    logits = (3 * torch.randn(N, V, device="cuda")).to(dtype).requires_grad_(True)
+    labels = torch.randint(0, V, (N, ), device="cuda")
+    labels[3] = -100
+    loss = DF.cross_entropy(logits, labels, inplace_backward=False)
+    lf = logits.detach().float().requires_grad_(True)
+    lr_ = F.cross_entropy(lf, labels, ignore_index=-100)
+    torch.testing.assert_close(loss.float(), lr_, rtol=1e-4, atol=1e-4)
+    loss.backward()
+    lr_.backward()
+    torch.testing.assert_close(logits.grad.float(), lf.grad, **TOL[dtype])

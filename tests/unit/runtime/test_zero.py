@@ -1,0 +1,69 @@
+"""ZeRO stages 0-3 vs a plain-PyTorch reference (reference strategy: `tests/unit/runtime/zero/test_zero.py`).
+
+Every rank trains the engine on its own micro-batches; the oracle is one process running torch.optim.AdamW over the
+concatenation of all ranks' batches with the same clipping, which is what data-parallel averaging must reproduce.
+"""
+import copy
+
+import pytest
+import torch
+
+from ..common import run_distributed
+from ..simple_model import base_config, random_tokens, tiny_llama
+
+
+def _reference_losses(world, steps, gas, mb, seq, lr, clip):
+    model = tiny_llama()
+    opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.01, eps=1e-8)
+    data = [random_tokens(steps * gas, mb, seq, seed=100 + r) for r in range(world)]
+    losses = []
+    for s in range(steps):
+        opt.zero_grad()
+        tot = 0.0
+        for a in range(gas):
+            for r in range(world):
+                x = data[r][s * gas + a]
+                loss = model(x, labels=x) / (gas * world)
+                loss.backward()
+                tot += float(loss)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
+        opt.step()
+        losses.append(tot)
+    return losses, {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+
+def _engine_run(stage, world, steps, gas, mb, seq, lr, clip, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    rank = dist.get_rank()
+    model = tiny_llama()
+    eng, _, _, _ = ds.initialize(model=model, config=base_config(stage=stage, lr=lr, mb=mb, gas=gas, clip=clip))
+    data = random_tokens(steps * gas, mb, seq, seed=100 + rank)
+    losses = []
+    for s in range(steps):
+        tot = torch.zeros(())
+        for a in range(gas):
+            x = data[s * gas + a]
+            loss = eng(x, labels=x)
+            eng.backward(loss)
+            eng.step()
+            tot += loss.detach() / gas
+        dist.all_reduce(tot)
+        losses.append(float(tot) / world)
+    sd = eng.module_state_dict()
+    if rank == 0:
+        torch.save({"losses": losses, "sd": sd}, out)
+
+
+@pytest.mark.parametrize("stage", [0, 1, 2, 3])
+@pytest.mark.parametrize("world,gas", [(1, 1), (2, 1), (2, 2)])
+def test_zero_matches_torch(stage, world, gas, tmp_path):
+    steps, mb, seq, lr, clip = 3, 2, 16, 1e-2, 1.0
+    out = str(tmp_path / "res.pt")
+    run_distributed(_engine_run, world, stage, world, steps, gas, mb, seq, lr, clip, out)
+    got = torch.load(out, weights_only=True)
+    ref_losses, ref_sd = _reference_losses(world, steps, gas, mb, seq, lr, clip)
+    assert got["losses"] == pytest.approx(ref_losses, rel=1e-4, abs=1e-5), (got["losses"], ref_losses)
+    for k, v in ref_sd.items():
+        if k in got["sd"]:
+            torch.testing.assert_close(got["sd"][k].float(), v.float(), rtol=1e-3, atol=2e-4, msg=k)
