@@ -58,18 +58,23 @@ class LlamaConfig:
         return 6 * self.num_params() + 12 * self.num_hidden_layers * self.hidden_size * seq_len
 
 
+def _mk(base, kw):
+    base.update(kw)
+    return LlamaConfig(**base)
+
+
 def llama2_7b_config(**kw):
-    return LlamaConfig(vocab_size=32000, hidden_size=4096, intermediate_size=11008, num_hidden_layers=32,
-                       num_attention_heads=32, num_key_value_heads=32, max_position_embeddings=4096, **kw)
+    return _mk(dict(vocab_size=32000, hidden_size=4096, intermediate_size=11008, num_hidden_layers=32,
+                    num_attention_heads=32, num_key_value_heads=32, max_position_embeddings=4096), kw)
 
 
 def llama2_13b_config(**kw):
-    return LlamaConfig(hidden_size=5120, intermediate_size=13824, num_hidden_layers=40, num_attention_heads=40, **kw)
+    return _mk(dict(hidden_size=5120, intermediate_size=13824, num_hidden_layers=40, num_attention_heads=40), kw)
 
 
 def llama2_70b_config(**kw):
-    return LlamaConfig(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
-                       num_key_value_heads=8, **kw)
+    return _mk(dict(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
+                    num_key_value_heads=8), kw)
 
 
 class RMSNorm(nn.Module):

@@ -66,12 +66,12 @@ class ParamCoordinator:
             self.ag_stream.wait_stream(compute)
             with self.acc.stream(self.ag_stream):
                 g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
-                dist.all_gather_into_tensor(g.full, g.shard, group=opt.dp_group)
+                dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
                 g.ag_event = self.acc.Event()
                 g.ag_event.record(self.ag_stream)
         else:
             g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
-            dist.all_gather_into_tensor(g.full, g.shard, group=opt.dp_group)
+            dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
             g.ag_event = None
         g.status = ZeroParamStatus.INFLIGHT
         self.live_numel += g.padded

@@ -62,8 +62,10 @@ class ZeroParamStatus:
 class FlatGroup:
     """A set of parameters sharing one flat buffer and one collective."""
 
-    def __init__(self, idx, params, dp, rank, partition, persistent, device, dtype, module=None):
+    def __init__(self, idx, params, dp, rank, partition, persistent, device, dtype, module=None, dp_group=None):
         self.idx = idx
+        self.dp_group = dp_group    # reduction / partition group (DP, or expert-DP for MoE experts)
+        self.reduce_dp = dp         # ranks that hold (a partition or a replica of) these params
         self.params = list(params)
         self.module = module
         self.dtype = dtype
@@ -130,6 +132,7 @@ class FlatZeroOptimizer:
         self.device = torch.device(self.acc.device_name(self.acc.current_device())) if self.acc.device_name() != "cpu" \
             else torch.device("cpu")
         self.partition = self.stage >= 1 and self.dp > 1
+        self.world = dist.get_world_size()
         self.comm_dtype = communication_data_type or dtype
         self.gas = gradient_accumulation_steps
         self.is_gradient_accumulation_boundary = True
@@ -182,6 +185,15 @@ class FlatZeroOptimizer:
         self.param_to_og = {id(p): og for p, og in plist}
         self.opt_params = [p for p, _ in plist]
         self.num_og = len(self.optimizer.param_groups)
+        # reduction group per optimizer group: MoE expert groups (marked {'moe': True, 'name': ep_size_k}) reduce and
+        # partition over their expert-data-parallel group, everything else over the (sequence x) data group
+        self.og_dp_group = []
+        for g in self.optimizer.param_groups:
+            if g.get("moe", False):
+                from ...parallel import groups as pgroups
+                self.og_dp_group.append(pgroups._get_expert_data_parallel_group(g["name"]))
+            else:
+                self.og_dp_group.append(self.dp_group)
         groups = []
         if self.stage == 3:
             # one group per module that directly owns trainable params (fetch granularity = module), plus ONE
@@ -221,8 +233,11 @@ class FlatZeroOptimizer:
                 groups.append(dict(params=cur, persistent=True, module=None))
         self.groups = []
         for i, d in enumerate(groups):
-            g = FlatGroup(i, d["params"], self.dp, self.rank, self.partition, d["persistent"], self.device,
-                          self.dtype, d["module"])
+            og = self.param_to_og[id(d["params"][0])]
+            pg = self.og_dp_group[og]
+            gdp, grank = dist.get_world_size(pg), dist.get_rank(pg)
+            g = FlatGroup(i, d["params"], gdp, grank, self.stage >= 1 and gdp > 1, d["persistent"] or gdp == 1,
+                          self.device, self.dtype, d["module"], dp_group=pg)
             self.groups.append(g)
         self.param_group = {}
         for g in self.groups:
@@ -407,18 +422,19 @@ class FlatZeroOptimizer:
             self.rs_stream.wait_stream(compute)
         with ctx:
             comm = src if src.dtype == self.comm_dtype else src.to(self.comm_dtype)
-            prescale = self.comm_dtype == torch.float16 and self.dp > 1
+            rdp = g.reduce_dp
+            prescale = self.comm_dtype == torch.float16 and rdp > 1
             if prescale:
-                comm.mul_(1.0 / self.dp)
-            if self.dp == 1:
+                comm.mul_(1.0 / rdp)
+            if rdp == 1:
                 out = comm[:g.seg]
-            elif self.partition:
+            elif g.partition:
                 out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
-                dist.reduce_scatter_tensor(out, comm, group=self.dp_group)
+                dist.reduce_scatter_tensor(out, comm, group=g.dp_group)
             else:
-                dist.all_reduce(comm, group=self.dp_group)
+                dist.all_reduce(comm, group=g.dp_group)
                 out = comm
-            alpha = 1.0 if (prescale or self.dp == 1) else 1.0 / self.dp
+            alpha = 1.0 if (prescale or rdp == 1) else 1.0 / rdp
             self._accumulate_runs(g, out, alpha)
             if not self._preset_mode():
                 # bucket memory is dead after the collective; let the allocator reuse it once rs_stream is done
@@ -479,21 +495,31 @@ class FlatZeroOptimizer:
     def _unscale_factor(self):
         return 1.0 / self.loss_scaler.loss_scale
 
+    def _og_replicas(self, og):
+        """Ranks holding an identical copy of each element of this og's local master (1 when partitioned)."""
+        pg = self.og_dp_group[og]
+        n = dist.get_world_size(pg)
+        return 1 if (self.stage >= 1 and n > 1) else n
+
     @torch.no_grad()
     def _global_norm_sq(self):
-        tensors = [t for t in self.grad_acc if t.numel() > 0]
-        if tensors and tensors[0].is_cuda:
-            sq = native.hip_ops().sumsq_multi(tensors)
-        else:
-            sq = sum((t.float().pow(2).sum() for t in tensors), torch.zeros((), device=self.device))
-        hs = [t for t in self.grad_acc_host if t is not None and t.numel() > 0]
-        if hs:
-            sq = sq + sum(t.pow(2).sum() for t in hs).to(sq.device)
-        if self.partition:
-            dist.all_reduce(sq, group=self.dp_group)
-        if self.mpu is not None and hasattr(self.mpu, "get_model_parallel_group") and \
-                self.mpu.get_model_parallel_world_size() > 1:
-            dist.all_reduce(sq, group=self.mpu.get_model_parallel_group())
+        """Squared global grad norm: each rank sums its unique elements (replicas divided out) and one all-reduce over
+        the world adds dense DP partitions, expert partitions and tensor-parallel shards alike."""
+        sq = torch.zeros((), dtype=torch.float32, device=self.device)
+        for og in range(self.num_og):
+            parts = [t for t in (self.grad_acc[og], self.grad_acc_host[og]) if t is not None and t.numel() > 0]
+            if not parts:
+                continue
+            dev = [t for t in parts if t.device.type != "cpu"]
+            s = native.hip_ops().sumsq_multi(dev) if dev and dev[0].is_cuda else \
+                sum((t.float().pow(2).sum() for t in parts if t.device.type == self.device.type),
+                    torch.zeros((), device=self.device))
+            host = [t for t in parts if t.device.type == "cpu" and self.device.type != "cpu"]
+            if host:
+                s = s + sum(t.pow(2).sum() for t in host).to(self.device)
+            sq = sq + s / self._og_replicas(og)
+        if self.world > 1:
+            dist.all_reduce(sq)
         return sq
 
     @torch.no_grad()
@@ -611,11 +637,9 @@ class FlatZeroOptimizer:
 
     def _post_step_gather(self):
         """Refresh full params of persistent groups from the updated shards (ZeRO-1/2, ZeRO-3 persistent)."""
-        if not self.partition:
-            return
         for g in self.groups:
-            if g.persistent and g.full is not None:
-                dist.all_gather_into_tensor(g.full, g.shard, group=self.dp_group)
+            if g.partition and g.persistent and g.full is not None:
+                dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
 
     def _zero_grad_buffers(self):
         for g in self.groups:
@@ -659,9 +683,9 @@ class FlatZeroOptimizer:
         for (s, e, og, moff, on_host) in g.runs:
             src = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
             seg32[s:e].copy_(src)
-        if self.partition:
+        if g.partition:
             full = torch.empty(g.padded, dtype=torch.float32, device=self.device)
-            dist.all_gather_into_tensor(full, seg32, group=self.dp_group)
+            dist.all_gather_into_tensor(full, seg32, group=g.dp_group)
         else:
             full = seg32
         return full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).clone()
@@ -678,8 +702,8 @@ class FlatZeroOptimizer:
                 dst = (self.master_host if on_host else self.master)[og]
                 dst[moff + x0 - lo:moff + x1 - lo].copy_(flat[x0 - a:x1 - a])
                 g.shard[x0 - g.seg_lo:x1 - g.seg_lo].copy_(flat[x0 - a:x1 - a])
-        if g.persistent and self.partition:
-            dist.all_gather_into_tensor(g.full, g.shard, group=self.dp_group)
+        if g.persistent and g.partition:
+            dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
 
     @torch.no_grad()
     def get_full_grad(self, p):
@@ -690,9 +714,9 @@ class FlatZeroOptimizer:
             src = (self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s]
             seg32[s:e].copy_(src)
         seg32.mul_(self._unscale_factor())
-        if self.partition:
+        if g.partition:
             full = torch.empty(g.padded, dtype=torch.float32, device=self.device)
-            dist.all_gather_into_tensor(full, seg32, group=self.dp_group)
+            dist.all_gather_into_tensor(full, seg32, group=g.dp_group)
         else:
             full = seg32
         return full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).clone()

@@ -193,7 +193,7 @@ class GatheredParameters:
                 if g.status != ZeroParamStatus.AVAILABLE:
                     opt = g._opt
                     full = torch.empty(g.padded, dtype=g.dtype, device=g.device)
-                    dist.all_gather_into_tensor(full, g.shard, group=opt.dp_group)
+                    dist.all_gather_into_tensor(full, g.shard, group=g.dp_group)
                     g.full = full
                     opt._point_params(g)
                     g.status = ZeroParamStatus.AVAILABLE
@@ -209,7 +209,7 @@ class GatheredParameters:
         if self.modifier_rank is not None:
             for p in self.params:
                 g = getattr(p, "ds_group", None)
-                grp = g._opt.dp_group if g is not None else getattr(p, "ds_process_group", None)
+                grp = g.dp_group if g is not None else getattr(p, "ds_process_group", None)
                 if dist.get_world_size(grp) > 1:
                     dist.broadcast(p.data, dist.get_global_rank(grp, self.modifier_rank), group=grp)
                 if g is not None:

@@ -36,7 +36,7 @@ def test_adam_flat(n, gdt, adamw):
     torch.testing.assert_close(p, pr, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(m, mr, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(v, vr, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(lp.float(), pr.bfloat16().float(), rtol=0, atol=0)
+    torch.testing.assert_close(lp.float(), p.bfloat16().float(), rtol=0, atol=0)
 
 
 def test_adam_flat_misaligned():
