@@ -183,7 +183,7 @@ std::vector<Tensor> rms_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, OptT dre
   auto dx = torch::empty_like(x);
   auto dw = torch::empty_like(w);
   const int nb = ds_norm_bwd_blocks(rows);
-  auto part = torch::empty({(int64_t)nb * H}, x.options().dtype(at::kFloat));
+  auto part = torch::empty({((int64_t)nb + 32) * H}, x.options().dtype(at::kFloat));
   if (dres.has_value()) need(*dres, "dres");
   check(ds_rms_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), ptr_or_null(dres),
                    dx.data_ptr(), dw.data_ptr(), part.data_ptr<float>(), rows, H, dcode(x), stream()),
@@ -214,7 +214,7 @@ std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rs
   auto dx = torch::empty_like(x);
   auto dg = torch::empty_like(g), db = torch::empty_like(g);
   const int nb = ds_norm_bwd_blocks(rows);
-  auto part = torch::empty({(int64_t)nb * 2 * H}, x.options().dtype(at::kFloat));
+  auto part = torch::empty({((int64_t)nb + 32) * 2 * H}, x.options().dtype(at::kFloat));
   check(ds_ln_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                   ptr_or_null(dres), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), part.data_ptr<float>(), rows, H,
                   dcode(x), stream()),

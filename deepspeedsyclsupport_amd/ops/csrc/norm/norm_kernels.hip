@@ -146,14 +146,31 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const T* __restrict__ dy, 
     dw_part[(int64_t)blockIdx.x * H + c] = sm[c] + sm[H + c] + sm[2 * H + c] + sm[3 * H + c];
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int nb, int H, int ld,
-                                                     T* __restrict__ out) {
+// Column sum of nb partial rows, two deterministic stages so the reduction uses the whole chip:
+// stage 1 (grid H/256 x CS): block (x, y) sums rows y, y+CS, ... of its 256 columns into stage[y][c];
+// stage 2 (grid H/256): sums the CS stage rows and casts.
+constexpr int CS = 32;
+__global__ void __launch_bounds__(256) colsum_stage1(const float* __restrict__ part, int nb, int H, int ld,
+                                                     float* __restrict__ stage) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= H) return;
   float acc = 0.f;
-  for (int b = 0; b < nb; ++b) acc += part[(int64_t)b * ld + c];
+  for (int b = blockIdx.y; b < nb; b += CS) acc += part[(int64_t)b * ld + c];
+  stage[(int64_t)blockIdx.y * H + c] = acc;
+}
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_stage2(const float* __restrict__ stage, int H, T* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= H) return;
+  float acc = 0.f;
+#pragma unroll
+  for (int y = 0; y < CS; ++y) acc += stage[(int64_t)y * H + c];
   out[c] = (T)acc;
+}
+template <typename T>
+static void colsum(const float* part, int nb, int H, int ld, float* stage, T* out, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_stage1, dim3((H + 255) / 256, CS), dim3(256), 0, s, part, nb, H, ld, stage);
+  hipLaunchKernelGGL((colsum_stage2<T>), dim3((H + 255) / 256), dim3(256), 0, s, stage, H, out);
 }
 
 // ------------------------------------------------------------------------------------------------ LayerNorm
@@ -321,7 +338,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
 static constexpr int kMaxHidden = 8192;
 static int norm_grid(int64_t rows) { return ds_grid_for((rows + 3) / 4, 1, 256 * 8); }
 
-// Number of fp32 partial rows the backward writes for `rows` (host allocates part[nb][H], [nb][2H] for LN).
+// Number of fp32 partial rows the backward writes for `rows`. The host allocates part[(nb + 32) * H] for RMSNorm
+// and part[(nb + 32) * 2H] for LayerNorm (the trailing 32 rows are the column-sum stage buffer).
 extern "C" int ds_norm_bwd_blocks(int64_t rows) { return ds_grid_for((rows + 3) / 4, 1, 512); }
 
 extern "C" int ds_rms_fwd(const void* x, const void* r, const void* w, void* y, void* res_out, float* rstd,
@@ -356,8 +374,7 @@ extern "C" int ds_rms_bwd(const void* dy, const void* x, const void* w, const fl
                          (const T*)w, rstd, nullptr, (T*)dx, part, rows, H);
   }));
   DS_CHECK_LAUNCH();
-  DISPATCH_T(dtype, hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, s, part, nb, H, H,
-                                       (T*)dw));
+  DISPATCH_T(dtype, colsum<T>(part, nb, H, H, part + (int64_t)nb * H, (T*)dw, s));
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -395,9 +412,10 @@ extern "C" int ds_ln_bwd(const void* dy, const void* x, const void* g, const flo
                          (const T*)g, mean, rstd, nullptr, (T*)dx, part, rows, H);
   }));
   DS_CHECK_LAUNCH();
+  float* stage = part + (int64_t)nb * 2 * H;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, s, part, nb, H, 2 * H, (T*)dg);
-    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, s, part + H, nb, H, 2 * H, (T*)db);
+    colsum<T>(part, nb, H, 2 * H, stage, (T*)dg, s);
+    colsum<T>(part + H, nb, H, 2 * H, stage + (int64_t)CS * H, (T*)db, s);
   });
   DS_CHECK_LAUNCH();
   return 0;

@@ -150,9 +150,16 @@ class DeepSpeedEngine(nn.Module):
     def _broadcast_model(self):
         if dist.get_world_size() == 1:
             return
+        from ..moe.utils import is_moe_param
         src = groups._get_broadcast_src_rank()
         for p in self.module.parameters():
-            if torch.is_tensor(p) and p.numel() > 0:
+            if not (torch.is_tensor(p) and p.numel() > 0):
+                continue
+            if is_moe_param(p):
+                # experts differ across EP ranks: replicate only within the expert-data-parallel group
+                dist.broadcast(p.data, groups._get_expert_broadcast_src_rank(p.group_name),
+                               group=groups._get_expert_data_parallel_group(p.group_name))
+            else:
                 dist.broadcast(p.data, src, group=self.seq_data_parallel_group)
 
     # ============================================================================================ optimizer
@@ -188,6 +195,19 @@ class DeepSpeedEngine(nn.Module):
         return cls(model_parameters, **params)
 
     def _configure_optimizer(self, client_optimizer, model_parameters):
+        from ..moe.utils import has_moe_layers, split_params_into_different_moe_groups_for_optimizer
+        self.has_moe_layers, self.num_experts = has_moe_layers(self.module)
+        if self.has_moe_layers:
+            if client_optimizer is None or not isinstance(client_optimizer, torch.optim.Optimizer):
+                mp = list(model_parameters)
+                if mp and torch.is_tensor(mp[0]):
+                    mp = [{"params": mp}]
+                model_parameters = split_params_into_different_moe_groups_for_optimizer(mp)
+            elif not any(g.get("moe", False) for g in client_optimizer.param_groups):
+                new = split_params_into_different_moe_groups_for_optimizer(client_optimizer.param_groups)
+                client_optimizer.param_groups = []
+                for g in new:
+                    client_optimizer.add_param_group(g)
         if client_optimizer is None:
             basic = self._configure_basic_optimizer(model_parameters)
         elif isinstance(client_optimizer, torch.optim.Optimizer):

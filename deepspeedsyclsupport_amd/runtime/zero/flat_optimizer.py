@@ -297,20 +297,16 @@ class FlatZeroOptimizer:
 
     @torch.no_grad()
     def _build_master(self):
-        """fp32 master / grad-accumulator buffers per optimizer group, as concatenated runs."""
+        """fp32 master buffers per optimizer group, as concatenated runs (rank-segment ∩ optimizer group)."""
         og_len = [0] * self.num_og
         run_specs = []
         for g in self.groups:
             ranges = g.param_seg_ranges(None)
-            # merge consecutive ranges of the same optimizer group (params are sorted by og within a group)
             runs = []
             for (i, s, e) in ranges:
                 og = self.param_to_og[id(g.params[i])]
-                if runs and runs[-1][2] == og and runs[-1][1] == s:
-                    runs[-1][1] = e
-                elif runs and runs[-1][2] == og:
-                    # gap = inter-param alignment padding: include it (it is zero and stays zero)
-                    runs[-1][1] = e
+                if runs and runs[-1][2] == og:
+                    runs[-1][1] = e  # contiguous or separated only by alignment padding (zero, stays zero)
                 else:
                     runs.append([s, e, og])
             for s, e, og in runs:
@@ -334,49 +330,61 @@ class FlatZeroOptimizer:
             g.runs.append((s - g.seg_lo, e - g.seg_lo, og, moff, on_host))
         pin = self.device.type == "cuda" and self.offload and getattr(self, "offload_pin", True)
         for og in range(self.num_og):
-            m = torch.zeros(dev_len[og], dtype=torch.float32, device=self.device)
-            self.master.append(m)
-            self.grad_acc.append(torch.zeros(dev_len[og], dtype=torch.float32, device=self.device))
-            hm = torch.zeros(host_len[og], dtype=torch.float32, pin_memory=pin) if host_len[og] else None
-            self.master_host.append(hm)
+            self.master.append(torch.zeros(dev_len[og], dtype=torch.float32, device=self.device))
+            self.grad_acc.append(None)  # fp32 accumulator, allocated only when a path needs it
+            self.master_host.append(torch.zeros(host_len[og], dtype=torch.float32, pin_memory=pin)
+                                    if host_len[og] else None)
             self.grad_acc_host.append(torch.zeros(host_len[og], dtype=torch.float32, pin_memory=pin)
                                       if host_len[og] else None)
-        # fill master from the bf16 shards
         for g in self.groups:
             for (s, e, og, moff, on_host) in g.runs:
                 dst = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
-                dst.copy_(g.shard[s:e].float())
+                dst.copy_(g.shard[s:e])
         # hand the fp32 buffers to the wrapped optimizer (its param_groups / lr schedule stay authoritative)
         self.fp32_flat = []
         for og, group in enumerate(self.optimizer.param_groups):
             mp = nn.Parameter(self.master[og], requires_grad=False)
-            mp.grad = self.grad_acc[og]
             self.fp32_flat.append(mp)
             group["params"] = [mp]
-        self.fp32_flat_host = []
-        for og in range(self.num_og):
-            if self.master_host[og] is not None:
-                hp = nn.Parameter(self.master_host[og], requires_grad=False)
-                hp.grad = self.grad_acc_host[og]
-                self.fp32_flat_host.append(hp)
-            else:
-                self.fp32_flat_host.append(None)
-        self.host_states = {}  # og -> (exp_avg, exp_avg_sq, step) for the Twin-Flow host part
-        self._grad_acc_valid = False
+        self.host_states = {}  # og -> [exp_avg, exp_avg_sq, step] for the Twin-Flow host part
+
+    def _ensure_grad_acc(self, og):
+        if self.grad_acc[og] is None:
+            self.grad_acc[og] = torch.zeros(self.master[og].numel(), dtype=torch.float32, device=self.device)
+        return self.grad_acc[og]
 
     # ================================================================================ gradient path
-    def _preset_mode(self):
-        """Grad views into persistent flat buffers (accumulated by autograd in place) vs copy-into-bucket."""
-        return self.stage <= 1 or self.dp == 1
+    # Per group the gradient lives in one of three places (chosen for the fewest HBM passes):
+    #   LOCAL  (no peer holds these params: dp == 1 for the group): autograd's own p.grad tensors feed the fused Adam
+    #          directly — no flat buffer, no copy, no zero-fill; accumulation across micro-steps is autograd's.
+    #   PRESET (ZeRO-0/1 with peers): p.grad are views into a persistent flat bf16 buffer that autograd accumulates into
+    #          in place; one reduce-scatter/all-reduce per group at the accumulation boundary; its output feeds Adam.
+    #   COPY   (ZeRO-2/3 with peers): the grad hook copies p.grad into a bucket and frees it; the bucket is reduced as
+    #          soon as the group is complete (overlapping the rest of backward); with GAS == 1 the reduced bf16
+    #          segment feeds Adam directly, with GAS > 1 it is accumulated into an fp32 partition.
+    LOCAL, PRESET, COPY = 0, 1, 2
+
+    def _mode(self, g):
+        if g.reduce_dp == 1:
+            return self.LOCAL
+        return self.PRESET if self.stage <= 1 else self.COPY
 
     def _install_grad_hooks(self):
         self._hooks = []
-        if self._preset_mode():
-            for g in self.groups:
+        for g in self.groups:
+            g.mode = self._mode(g)
+            g.red_out = None
+            g._acc_valid = False
+            if g.mode == self.PRESET:
                 g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
                 self._point_grads(g)
         for p in self.opt_params:
-            self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_ready_hook))
+            g, _ = self.param_group[id(p)]
+            if g.mode != self.LOCAL or self.coordinator_needed():
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_ready_hook))
+
+    def coordinator_needed(self):
+        return self.stage == 3 and any(not g.persistent for g in self.groups)
 
     def _point_grads(self, g):
         for i, p in enumerate(g.params):
@@ -389,27 +397,35 @@ class FlatZeroOptimizer:
 
     def _grad_ready_hook(self, p):
         g, i = self.param_group[id(p)]
-        if self._preset_mode():
+        if g.mode == self.PRESET:
             view = g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]]
             if p.grad is None or p.grad.data_ptr() != view.data_ptr():
-                # someone reset p.grad (e.g. module.zero_grad(set_to_none=True)): fold it back into the flat buffer
+                # p.grad was reset (e.g. module.zero_grad(set_to_none=True)): fold it back into the flat buffer
                 if p.grad is not None:
                     view.add_(p.grad.reshape(-1))
                 p.grad = view.view(p.ds_shape)
-        else:
+        elif g.mode == self.COPY:
             if g.grad_flat is None:
                 g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
             g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1))
             p.grad = None
         g.pending -= 1
-        if g.pending == 0 and self._should_reduce_now():
+        if g.pending == 0 and g.mode != self.LOCAL and self._should_reduce_now():
             self._reduce_group(g)
         if self.coordinator is not None and g.pending == 0 and not g.persistent:
             self.coordinator.release_after_backward(g)
 
     def _should_reduce_now(self):
-        # ZeRO-1 / no-ZeRO accumulate locally and reduce only at the accumulation boundary
+        # ZeRO-0/1 accumulate locally and reduce only at the accumulation boundary
         return self.is_gradient_accumulation_boundary or self.stage >= 2
+
+    def _div(self):
+        # gradient = mean over the GLOBAL batch (dense DP size), for expert groups too; the reference divides expert
+        # grads by the expert-DP size only (an ep-times larger scale, `stage_1_and_2.py` average_tensor)
+        return float(self.dp)
+
+    def _prescale(self):
+        return self.comm_dtype == torch.float16 and self._div() > 1
 
     def _reduce_group(self, g):
         if g.reduced_this_pass:
@@ -422,47 +438,44 @@ class FlatZeroOptimizer:
             self.rs_stream.wait_stream(compute)
         with ctx:
             comm = src if src.dtype == self.comm_dtype else src.to(self.comm_dtype)
-            rdp = g.reduce_dp
-            prescale = self.comm_dtype == torch.float16 and rdp > 1
-            if prescale:
-                comm.mul_(1.0 / rdp)
-            if rdp == 1:
-                out = comm[:g.seg]
-            elif g.partition:
+            if self._prescale():
+                comm.mul_(1.0 / self._div())
+            if g.partition:
                 out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
                 dist.reduce_scatter_tensor(out, comm, group=g.dp_group)
             else:
                 dist.all_reduce(comm, group=g.dp_group)
-                out = comm
-            alpha = 1.0 if (prescale or rdp == 1) else 1.0 / rdp
-            self._accumulate_runs(g, out, alpha)
-            if not self._preset_mode():
-                # bucket memory is dead after the collective; let the allocator reuse it once rs_stream is done
+                out = comm[g.seg_lo:g.seg_lo + g.seg]
+            if g.mode == self.COPY and self.gas > 1:
+                self._accumulate_runs(g, out, self._alpha())
+            else:
+                g.red_out = out
+            if g.mode == self.COPY:
                 if self.rs_stream is not None:
                     src.record_stream(self.rs_stream)
                 g.grad_flat = None
 
+    def _alpha(self):
+        return 1.0 if (self._prescale() or self._div() == 1) else 1.0 / self._div()
+
     def _accumulate_runs(self, g, seg_grad, alpha):
-        first = not self._grad_acc_valid_for(g)
+        first = not g._acc_valid
         for (s, e, og, moff, on_host) in g.runs:
             src = seg_grad[s:e]
             if on_host:
                 dst = self.grad_acc_host[og][moff:moff + e - s]
-                tmp = src.float().mul_(alpha) if alpha != 1.0 else src.float()
+                tmp = src.float().mul_(alpha).cpu()
                 if first:
-                    dst.copy_(tmp, non_blocking=True)
+                    dst.copy_(tmp)
                 else:
-                    dst.add_(tmp.cpu())
+                    dst.add_(tmp)
             else:
-                dst = self.grad_acc[og][moff:moff + e - s]
+                dst = self._ensure_grad_acc(og)[moff:moff + e - s]
                 if first:
                     torch.mul(src, alpha, out=dst) if alpha != 1.0 else dst.copy_(src)
                 else:
                     dst.add_(src, alpha=alpha)
         g._acc_valid = True
-
-    def _grad_acc_valid_for(self, g):
-        return getattr(g, "_acc_valid", False)
 
     def backward_prologue(self):
         self._begin_pass()
@@ -481,7 +494,7 @@ class FlatZeroOptimizer:
         """Flush groups whose params got no grad this pass (unused params count as zero) and join streams."""
         if self._should_reduce_now():
             for g in self.groups:
-                if not g.reduced_this_pass:
+                if g.mode != self.LOCAL and not g.reduced_this_pass:
                     if g.grad_flat is None:
                         g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
                     self._reduce_group(g)
@@ -501,23 +514,43 @@ class FlatZeroOptimizer:
         n = dist.get_world_size(pg)
         return 1 if (self.stage >= 1 and n > 1) else n
 
+    def _grad_items(self):
+        """[(og, moff, n, grad_1d, lp_1d, scale, on_host)] covering every local master element that has a gradient."""
+        items = []
+        alpha = self._alpha()
+        div = self._div()
+        for g in self.groups:
+            for (s, e, og, moff, on_host) in g.runs:
+                if g.mode == self.LOCAL:
+                    for i, p in enumerate(g.params):
+                        a, n = g.offsets[i], g.numels[i]
+                        lo, hi = max(a, g.seg_lo + s), min(a + n, g.seg_lo + e)
+                        if lo >= hi or p.grad is None:
+                            continue
+                        gr = p.grad.reshape(-1)[lo - a:hi - a]
+                        items.append((og, moff + lo - g.seg_lo - s, hi - lo, gr, g.shard[lo - g.seg_lo:hi - g.seg_lo],
+                                      1.0 / div, on_host))
+                elif g._acc_valid:
+                    src = (self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s]
+                    items.append((og, moff, e - s, src, g.shard[s:e], 1.0, on_host))
+                elif g.red_out is not None:
+                    items.append((og, moff, e - s, g.red_out[s:e], g.shard[s:e], alpha, on_host))
+        return items
+
     @torch.no_grad()
-    def _global_norm_sq(self):
-        """Squared global grad norm: each rank sums its unique elements (replicas divided out) and one all-reduce over
+    def _global_norm_sq(self, items):
+        """Squared global grad norm: each rank sums its unique elements (replicas divided out) and ONE all-reduce over
         the world adds dense DP partitions, expert partitions and tensor-parallel shards alike."""
+        classes = defaultdict(list)
+        for (og, moff, n, gr, lp, scale, on_host) in items:
+            classes[(og, scale, gr.device.type)].append(gr)
         sq = torch.zeros((), dtype=torch.float32, device=self.device)
-        for og in range(self.num_og):
-            parts = [t for t in (self.grad_acc[og], self.grad_acc_host[og]) if t is not None and t.numel() > 0]
-            if not parts:
-                continue
-            dev = [t for t in parts if t.device.type != "cpu"]
-            s = native.hip_ops().sumsq_multi(dev) if dev and dev[0].is_cuda else \
-                sum((t.float().pow(2).sum() for t in parts if t.device.type == self.device.type),
-                    torch.zeros((), device=self.device))
-            host = [t for t in parts if t.device.type == "cpu" and self.device.type != "cpu"]
-            if host:
-                s = s + sum(t.pow(2).sum() for t in host).to(self.device)
-            sq = sq + s / self._og_replicas(og)
+        for (og, scale, devtype), ts in classes.items():
+            if devtype == "cuda":
+                s = native.hip_ops().sumsq_multi([t.contiguous() for t in ts])
+            else:
+                s = sum((t.float().pow(2).sum() for t in ts), torch.zeros(())).to(self.device)
+            sq = sq + s * (scale * scale) / self._og_replicas(og)
         if self.world > 1:
             dist.all_reduce(sq)
         return sq
@@ -525,11 +558,10 @@ class FlatZeroOptimizer:
     @torch.no_grad()
     def step(self, closure=None, lr_kwargs=None):
         """Optimizer step at the accumulation boundary (the engine only calls it there)."""
+        items = self._grad_items()
         scale = self._unscale_factor()
-        norm_sq = self._global_norm_sq()
-        norm = norm_sq.sqrt() * scale
-        # one device->host sync per step for overflow / clipping decisions
-        norm_f = float(norm)
+        norm = self._global_norm_sq(items).sqrt() * scale
+        norm_f = float(norm)  # the one device->host sync per step (overflow / clipping decisions)
         self._global_grad_norm = norm_f
         overflow = not math.isfinite(norm_f)
         self.overflow = overflow
@@ -544,12 +576,14 @@ class FlatZeroOptimizer:
         if self.clip_grad and self.clip_grad > 0 and norm_f > self.clip_grad:
             clip = self.clip_grad / (norm_f + 1e-6)
         grad_scale = scale * clip
+        host_items = [it for it in items if it[6]]
         host_thread = None
-        if self.offload and any(t is not None for t in self.master_host):
+        if host_items:
+            self._stage_host_grads(host_items)
             import threading
             host_thread = threading.Thread(target=self._host_step, args=(grad_scale, ))
             host_thread.start()
-        self._device_step(grad_scale)
+        self._device_step([it for it in items if not it[6]], grad_scale)
         if host_thread is not None:
             host_thread.join()
             self._host_writeback()
@@ -557,58 +591,80 @@ class FlatZeroOptimizer:
         self._zero_grad_buffers()
         self.global_steps += 1
 
-    def _device_step(self, grad_scale):
+    def _stage_host_grads(self, host_items):
+        for (og, moff, n, gr, lp, s, on_host) in host_items:
+            if gr.device.type == "cpu" and gr.data_ptr() == self.grad_acc_host[og][moff:moff + n].data_ptr():
+                if s != 1.0:
+                    gr.mul_(s)
+                continue
+            self.grad_acc_host[og][moff:moff + n].copy_((gr.float() * s), non_blocking=True)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+
+    def _device_step(self, items, grad_scale):
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
         if self._fused_adam:
+            by_og = defaultdict(list)
+            for it in items:
+                by_og[it[0]].append(it)
             for og, group in enumerate(self.optimizer.param_groups):
                 fp = self.fp32_flat[og]
-                if fp.numel() == 0:
-                    continue
                 st = self.optimizer.state[fp]
                 if len(st) == 0:
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(fp.data)
                     st["exp_avg_sq"] = torch.zeros_like(fp.data)
                 st["step"] += 1
+                if fp.numel() == 0 or not by_og.get(og):
+                    continue
                 b1, b2 = group["betas"]
                 step = st["step"]
-                bc1 = 1 - b1**step if group.get("bias_correction", True) else 1.0
-                bc2 = 1 - b2**step if group.get("bias_correction", True) else 1.0
-                ps, ms, vs, gs, lps = [], [], [], [], []
-                for g in self.groups:
-                    for (s, e, og2, moff, on_host) in g.runs:
-                        if og2 != og or on_host:
-                            continue
-                        n = e - s
-                        ps.append(fp.data[moff:moff + n])
-                        ms.append(st["exp_avg"][moff:moff + n])
-                        vs.append(st["exp_avg_sq"][moff:moff + n])
-                        gs.append(self.grad_acc[og][moff:moff + n])
-                        lps.append(g.shard[s:e])
-                adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
-                if fp.is_cuda:
-                    native.hip_ops().adam_multi(ps, ms, vs, gs, lps, group["lr"], b1, b2, group["eps"],
-                                                group["weight_decay"], bc1, bc2, grad_scale, adamw)
-                else:
-                    from ...ops import reference
-                    for p_, m_, v_, g_, lp_ in zip(ps, ms, vs, gs, lps):
-                        reference.adam_update(p_, m_, v_, g_, group["lr"], b1, b2, group["eps"],
-                                              group["weight_decay"], step, group.get("bias_correction", True), adamw,
-                                              grad_scale, lp_)
+                bc = group.get("bias_correction", True)
+                bc1 = 1 - b1**step if bc else 1.0
+                bc2 = 1 - b2**step if bc else 1.0
+                # one multi-tensor launch per (grad dtype, grad scale) class
+                classes = defaultdict(list)
+                for (_, moff, n, gr, lp, s, _h) in by_og[og]:
+                    classes[(gr.dtype, s)].append((moff, n, gr, lp))
+                for (gdt, s), lst in classes.items():
+                    ps = [fp.data[moff:moff + n] for moff, n, _, _ in lst]
+                    ms = [st["exp_avg"][moff:moff + n] for moff, n, _, _ in lst]
+                    vs = [st["exp_avg_sq"][moff:moff + n] for moff, n, _, _ in lst]
+                    gs = [gr for _, _, gr, _ in lst]
+                    lps = [lp for _, _, _, lp in lst]
+                    if fp.is_cuda:
+                        native.hip_ops().adam_multi(ps, ms, vs, gs, lps, group["lr"], b1, b2, group["eps"],
+                                                    group["weight_decay"], bc1, bc2, grad_scale * s, adamw)
+                    else:
+                        from ...ops import reference
+                        for p_, m_, v_, g_, lp_ in zip(ps, ms, vs, gs, lps):
+                            reference.adam_update(p_, m_, v_, g_, group["lr"], b1, b2, group["eps"],
+                                                  group["weight_decay"], step, bc, adamw, grad_scale * s, lp_)
         else:
-            # generic torch optimizer over the fp32 flats: unscale/clip grads in place, step, copy to shards
+            # generic torch optimizer over the fp32 flats: materialise scaled fp32 grads, step, copy to shards
             for og in range(self.num_og):
-                if grad_scale != 1.0:
-                    self.grad_acc[og].mul_(grad_scale)
+                self._ensure_grad_acc(og)
+            touched = set()
+            for (og, moff, n, gr, lp, s, _h) in items:
+                dst = self.grad_acc[og][moff:moff + n]
+                if dst.data_ptr() == gr.data_ptr():
+                    dst.mul_(grad_scale)
+                else:
+                    torch.mul(gr, grad_scale * s, out=dst) if gr.dtype == torch.float32 else \
+                        dst.copy_(gr).mul_(grad_scale * s)
+                touched.add(og)
+            for og in range(self.num_og):
+                self.fp32_flat[og].grad = self.grad_acc[og]
             self.optimizer.step()
-            for g in self.groups:
-                for (s, e, og, moff, on_host) in g.runs:
-                    if not on_host:
-                        g.shard[s:e].copy_(self.master[og][moff:moff + e - s])
+            for (og, moff, n, gr, lp, s, _h) in items:
+                lp.copy_(self.master[og][moff:moff + n])
 
     def _host_step(self, grad_scale):
-        """Twin-Flow host half: native CPU Adam on pinned fp32 partitions (runs on a worker thread)."""
+        """Twin-Flow host half: native CPU Adam on pinned fp32 partitions (runs on a worker thread, concurrently
+        with the device Adam launched on the main thread)."""
         from ...ops.native import cpu_ops
-        torch.cuda.synchronize() if self.device.type == "cuda" else None
+        if not hasattr(self, "_host_lp"):
+            self._host_lp = {}
         for og, group in enumerate(self.optimizer.param_groups):
             hp = self.master_host[og]
             if hp is None:
@@ -619,8 +675,6 @@ class FlatZeroOptimizer:
                 self.host_states[og] = st
             st[2] += 1
             b1, b2 = group["betas"]
-            if not hasattr(self, "_host_lp"):
-                self._host_lp = {}
             lp = self._host_lp.get(og)
             if lp is None:
                 lp = torch.empty(hp.numel(), dtype=self.dtype, pin_memory=self.device.type == "cuda")
@@ -644,12 +698,16 @@ class FlatZeroOptimizer:
     def _zero_grad_buffers(self):
         for g in self.groups:
             g._acc_valid = False
-            if self._preset_mode() and g.grad_flat is not None:
+            g.red_out = None
+            if g.mode == self.PRESET and g.grad_flat is not None:
                 g.grad_flat.zero_()
+            elif g.mode == self.LOCAL:
+                for p in g.params:
+                    p.grad = None
         self.micro_step = 0
 
     def zero_grad(self, set_to_none=True):
-        # grads live in the flat buffers; user-visible p.grad views are kept (preset mode) or None (copy mode)
+        # gradients are owned by the optimizer between backward and step (see gradient-path comment)
         pass
 
     # ================================================================================ accessors / compat
@@ -710,9 +768,14 @@ class FlatZeroOptimizer:
         """Averaged fp32 gradient of one param (valid between backward at the boundary and step)."""
         g, i = self.param_group[id(p)]
         seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
-        for (s, e, og, moff, on_host) in g.runs:
-            src = (self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s]
-            seg32[s:e].copy_(src)
+        if g.mode == self.LOCAL:
+            if p.grad is not None:
+                seg32[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1)).mul_(1.0 / self._div())
+        elif g._acc_valid:
+            for (s, e, og, moff, on_host) in g.runs:
+                seg32[s:e].copy_((self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s])
+        elif g.red_out is not None:
+            seg32.copy_(g.red_out).mul_(self._alpha())
         seg32.mul_(self._unscale_factor())
         if g.partition:
             full = torch.empty(g.padded, dtype=torch.float32, device=self.device)

@@ -1,0 +1,105 @@
+"""MoE / expert parallelism (reference `tests/unit/moe/test_moe.py`): EP=2 over gloo vs single-process with both
+experts local (drop_tokens=False so routing is capacity-free and deterministic)."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+from ..common import run_distributed
+
+H, E, STEPS = 16, 2, 3
+
+
+class MoEModel(nn.Module):
+
+    def __init__(self, ep_size, k=1):
+        super().__init__()
+        from deepspeedsyclsupport_amd.moe import MoE
+        torch.manual_seed(0)
+        self.inp = nn.Linear(H, H)
+        expert = nn.Sequential(nn.Linear(H, 2 * H), nn.GELU(), nn.Linear(2 * H, H))
+        self.moe = MoE(H, expert, num_experts=E, ep_size=ep_size, k=k, drop_tokens=False, use_rts=False)
+        self.out = nn.Linear(H, 4)
+
+    def forward(self, x, y):
+        h, l_aux, _ = self.moe(torch.relu(self.inp(x)))
+        return nn.functional.cross_entropy(self.out(h), y)
+
+
+def _data(rank):
+    g = torch.Generator().manual_seed(10 + rank)
+    return [(torch.randn(6, H, generator=g), torch.randint(0, 4, (6, ), generator=g)) for _ in range(STEPS)]
+
+
+def _ep_run(k, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.moe.utils import is_moe_param
+    model = MoEModel(ep_size=2, k=k)
+    rank = dist.get_rank()
+    # expert e of the reference lives on rank e: load the matching reference expert weights
+    ref = MoEModel(ep_size=1, k=k)
+    with torch.no_grad():
+        refp = dict(ref.named_parameters())
+        for n, p in model.named_parameters():
+            if "deepspeed_experts" in n:
+                src = ref.moe.deepspeed_moe.experts.deepspeed_experts[rank]
+                sub = n.split("deepspeed_experts.0.")[1]
+                p.copy_(dict(src.named_parameters())[sub])
+            else:
+                p.copy_(refp[n])
+    cfg = {"train_micro_batch_size_per_gpu": 6, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}},
+           "zero_optimization": {"stage": 1}, "gradient_clipping": 0.0}
+    eng, _, _, _ = ds.initialize(model=model, config=cfg)
+    losses = []
+    for x, y in _data(rank):
+        loss = eng(x, y)
+        eng.backward(loss)
+        eng.step()
+        t = loss.detach().clone()
+        dist.all_reduce(t)
+        losses.append(float(t) / 2)
+    if rank == 0:
+        torch.save(losses, out)
+
+
+def _ref_losses(k):
+    model = MoEModel(ep_size=1, k=k)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01)
+    d0, d1 = _data(0), _data(1)
+    losses = []
+    for (x0, y0), (x1, y1) in zip(d0, d1):
+        opt.zero_grad()
+        loss = (model(x0, y0) + model(x1, y1)) / 2
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    return losses
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_moe_expert_parallel_matches_local(k, tmp_path):
+    out = str(tmp_path / "l.pt")
+    run_distributed(_ep_run, 2, k, out)
+    got = torch.load(out)
+    ref = _ref_losses(k)
+    assert got == pytest.approx(ref, rel=1e-4, abs=1e-5), (got, ref)
+
+
+def test_gating_capacity_and_aux_loss():
+    from deepspeedsyclsupport_amd.moe.sharded_moe import _route
+    torch.manual_seed(0)
+    logits = torch.randn(64, 4)
+    l_aux, idx, loc, w, cap, counts = _route(logits, 1, 1.0, 4, None, True, False, None, training=False)
+    assert cap == 16
+    for e in range(4):
+        locs = loc[:, 0][idx[:, 0] == e]
+        kept = locs[locs >= 0]
+        assert kept.numel() == min(int((idx[:, 0] == e).sum()), cap)
+        assert sorted(kept.tolist()) == list(range(kept.numel()))
+    assert float(l_aux) > 0
+    l2, idx2, loc2, w2, cap2, _ = _route(logits, 2, 1.0, 4, None, True, False, None, False, training=False)
+    assert torch.all(idx2[:, 0] != idx2[:, 1])
+    both = (loc2 >= 0).all(1)
+    torch.testing.assert_close(w2[both].sum(1), torch.ones(int(both.sum())))
