@@ -38,13 +38,13 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
     assert config is not None, "DeepSpeed requires --deepspeed_config or config=..."
     if dist_init_required is not False:
         init_distributed(dist_init_required=dist_init_required)
-    cfg = config if isinstance(config, DeepSpeedConfig) else DeepSpeedConfig(config, mpu)
-    pipe = False
     try:
         from .runtime.pipe.module import PipelineModule
         pipe = isinstance(model, PipelineModule)
-    except Exception:
+    except ImportError:
         pipe = False
+    cfg = config if isinstance(config, DeepSpeedConfig) else \
+        DeepSpeedConfig(config, model.mpu() if pipe else mpu)
     if pipe:
         from .runtime.pipe.engine import PipelineEngine
         engine = PipelineEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,

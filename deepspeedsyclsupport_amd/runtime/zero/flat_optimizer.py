@@ -504,6 +504,18 @@ class FlatZeroOptimizer:
             self.coordinator.end_backward()
         self.micro_step += 1
 
+    def reduce_gradients(self, pipeline_parallel=False):
+        """Boundary reduction issued explicitly (pipeline engine: after tied-weight gradients were summed)."""
+        self.is_gradient_accumulation_boundary = True
+        for g in self.groups:
+            if g.mode != self.LOCAL:
+                g.reduced_this_pass = False
+                if g.grad_flat is None:
+                    g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
+                self._reduce_group(g)
+        if self.rs_stream is not None:
+            self.acc.current_stream().wait_stream(self.rs_stream)
+
     # ================================================================================ step
     def _unscale_factor(self):
         return 1.0 / self.loss_scaler.loss_scale
