@@ -28,7 +28,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-13b", "tiny"])
     ap.add_argument("--seq-len", type=int, default=4096)
-    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("DS_BENCH_MB", "4")))
+    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("DS_BENCH_MB", "8")))
     ap.add_argument("--gas", type=int, default=1)
     ap.add_argument("--stage", type=int, default=3)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing (not needed with 288 GB HBM)")

@@ -1,0 +1,394 @@
+"""Kernel-injected inference transformer (reference v1 `model_implementations/transformers/ds_transformer.py`,
+`ops/transformer/inference/{ds_attention.py, ds_mlp.py}` and the v2 model implementations).
+
+One decoder-layer implementation parametrised by `DSModelSpec` covers the architectures the reference injects
+(Llama/Llama-2/Mistral/Qwen2, GPT-2, BLOOM, OPT, GPT-NeoX): norm type, positional scheme (rotary-half, rotary
+GPT-J, ALiBi, learned), gated or plain MLP, biases, parallel residual. Hot path per layer:
+  fused (residual +) norm -> QKV GEMM (hipBLASLt) -> RoPE (HIP) -> KV append into the blocked cache (HIP) ->
+  attention: prefill = SDPA, decode = paged flash-decoding kernel (HIP) -> O GEMM -> TP all-reduce ->
+  fused residual + norm -> MLP GEMM -> fused gated activation (HIP) -> GEMM -> TP all-reduce.
+Tensor parallelism is column-parallel QKV/FC1 (sharded by heads / intermediate), row-parallel O/FC2 with one RCCL
+all-reduce each (bias added once after it), vocab-parallel LM head with an all-gather of logits.
+Weight-only int8/int4 quantisation keeps group-quantised weights and dequantises into a per-layer workspace.
+"""
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ... import comm as dist
+from ...ops import reference
+from ...ops.transformer import functional as DF
+
+
+@dataclass
+class DSModelSpec:
+    arch: str
+    vocab_size: int
+    hidden_size: int
+    num_layers: int
+    num_heads: int
+    num_kv_heads: int
+    intermediate_size: int
+    head_dim: int = 0
+    norm: str = "rms"                # "rms" | "ln"
+    norm_eps: float = 1e-5
+    pos: str = "rope"                # "rope" | "rope_gptj" | "alibi" | "learned" | "none"
+    rope_theta: float = 10000.0
+    rotary_dim: int = 0
+    act: str = "silu"                # activation name (ACT_CODES)
+    gated_mlp: bool = True
+    qkv_bias: bool = False
+    o_bias: bool = False
+    mlp_bias: bool = False
+    parallel_residual: bool = False
+    shared_parallel_norm: bool = False  # GPT-J style single norm for attn+mlp
+    embed_norm: bool = False         # BLOOM word_embeddings_layernorm
+    final_norm: bool = True
+    tie_embeddings: bool = False
+    max_positions: int = 4096
+    learned_pos_offset: int = 0      # OPT uses 2
+    sliding_window: int = 0
+    lm_head_bias: bool = False
+
+    def __post_init__(self):
+        if not self.head_dim:
+            self.head_dim = self.hidden_size // self.num_heads
+        if not self.rotary_dim:
+            self.rotary_dim = self.head_dim
+
+
+def alibi_slopes(n_heads):
+    closest = 2**math.floor(math.log2(n_heads))
+    base = 2**(-(2**-(math.log2(closest) - 3)))
+    slopes = [base**i for i in range(1, closest + 1)]
+    if closest != n_heads:
+        extra_base = 2**(-(2**-(math.log2(2 * closest) - 3)))
+        n_rem = min(closest, n_heads - closest)
+        slopes += [extra_base**i for i in range(1, 2 * n_rem + 1, 2)]
+    return torch.tensor(slopes, dtype=torch.float32)
+
+
+class QuantLinearWeight:
+    """Group-quantised weight (int8/int4) dequantised into a shared workspace right before its GEMM."""
+
+    def __init__(self, w, bits=8, group_size=64):
+        from ...ops.quantizer import quantize
+        self.shape = w.shape
+        self.dtype = w.dtype
+        self.qt = quantize(w, group_size=min(group_size, w.numel()), bits=bits, symmetric=True)
+
+    def materialize(self):
+        from ...ops.quantizer import dequantize
+        return dequantize(self.qt, self.dtype)
+
+
+def _weight(w):
+    return w.materialize() if isinstance(w, QuantLinearWeight) else w
+
+
+@dataclass
+class BatchMeta:
+    block_tables: torch.Tensor       # [B, max_blocks] int32 (device)
+    start_pos: torch.Tensor          # [B] int32 tokens already cached
+    seq_lens: torch.Tensor           # [B] int32 = start_pos + n_new
+    pos_ids: torch.Tensor            # [B*n_new] int32 absolute positions
+    n_new: int
+    max_len: int                     # host upper bound of seq_lens (kernel split sizing)
+    prefill_from_zero: bool          # every sequence starts at position 0 (pure prefill)
+
+
+class DSInferenceLayer(nn.Module):
+
+    def __init__(self, spec: DSModelSpec, layer_idx: int, tp_group=None, tp_size=1, dtype=torch.bfloat16,
+                 device=None):
+        super().__init__()
+        self.spec = spec
+        self.layer_idx = layer_idx
+        self.tp_group = tp_group
+        self.tp = tp_size
+        assert spec.num_heads % tp_size == 0, "heads must divide tp size"
+        self.hq = spec.num_heads // tp_size
+        self.hk = max(spec.num_kv_heads // tp_size, 1)
+        D = spec.head_dim
+        H = spec.hidden_size
+        I = spec.intermediate_size // tp_size
+        kw = dict(dtype=dtype, device=device)
+        self.ln1_w = nn.Parameter(torch.ones(H, **kw), requires_grad=False)
+        self.ln1_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.norm == "ln" else None
+        self.ln2_w = nn.Parameter(torch.ones(H, **kw), requires_grad=False)
+        self.ln2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.norm == "ln" else None
+        self.qkv_w = nn.Parameter(torch.empty((self.hq + 2 * self.hk) * D, H, **kw), requires_grad=False)
+        self.qkv_b = nn.Parameter(torch.zeros((self.hq + 2 * self.hk) * D, **kw), requires_grad=False) \
+            if spec.qkv_bias else None
+        self.o_w = nn.Parameter(torch.empty(H, self.hq * D, **kw), requires_grad=False)
+        self.o_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.o_bias else None
+        self.fc1_w = nn.Parameter(torch.empty((2 if spec.gated_mlp else 1) * I, H, **kw), requires_grad=False)
+        self.fc1_b = nn.Parameter(torch.zeros((2 if spec.gated_mlp else 1) * I, **kw), requires_grad=False) \
+            if spec.mlp_bias else None
+        self.fc2_w = nn.Parameter(torch.empty(H, I, **kw), requires_grad=False)
+        self.fc2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.mlp_bias else None
+        self.quant = {}
+
+    # ------------------------------------------------------------------------------------------ helpers
+    def quantize_weights(self, bits=8, group_size=64):
+        for name in ("qkv_w", "o_w", "fc1_w", "fc2_w"):
+            self.quant[name] = QuantLinearWeight(getattr(self, name).data, bits, group_size)
+            getattr(self, name).data = torch.empty(0, dtype=getattr(self, name).dtype,
+                                                   device=getattr(self, name).device)
+
+    def _w(self, name):
+        return self.quant[name].materialize() if name in self.quant else getattr(self, name)
+
+    def _norm(self, x, w, b, residual=None):
+        if self.spec.norm == "rms":
+            return DF.rms_norm(x, w, self.spec.norm_eps, residual)
+        return DF.layer_norm(x, w, b, self.spec.norm_eps, residual)
+
+    def _allreduce(self, x):
+        if self.tp > 1:
+            dist.inference_all_reduce(x, group=self.tp_group)
+        return x
+
+    # ------------------------------------------------------------------------------------------ attention
+    def _attention(self, x, meta: BatchMeta, cache, rope, alibi):
+        spec = self.spec
+        B = x.shape[0]
+        n = meta.n_new
+        D = spec.head_dim
+        qkv = F.linear(x, self._w("qkv_w"), self.qkv_b).view(B, n, self.hq + 2 * self.hk, D)
+        q, k, v = qkv.split([self.hq, self.hk, self.hk], dim=2)
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        if spec.pos in ("rope", "rope_gptj"):
+            inter = spec.pos == "rope_gptj"
+            DF.apply_rotary_pos_emb(q, rope[0], rope[1], position_ids=meta.pos_ids.view(B, n), rotary_dim=spec.rotary_dim,
+                                    interleaved=inter)
+            DF.apply_rotary_pos_emb(k, rope[0], rope[1], position_ids=meta.pos_ids.view(B, n), rotary_dim=spec.rotary_dim,
+                                    interleaved=inter)
+        kc, vc = cache.k[self.layer_idx], cache.v[self.layer_idx]
+        _kv_append(k, v, kc, vc, meta)
+        scale = 1.0 / math.sqrt(D)
+        if meta.prefill_from_zero and n > 1:
+            o = _prefill_attention(q, k, v, scale, alibi, spec.sliding_window)
+        elif n == 1:
+            o = _decode_attention(q.view(B, self.hq, D), kc, vc, meta, scale, alibi, spec.sliding_window)
+            o = o.view(B, 1, self.hq, D)
+        else:
+            o = _cached_attention(q, kc, vc, meta, scale, alibi, spec.sliding_window)
+        o = o.reshape(B, n, self.hq * D)
+        out = F.linear(o, self._w("o_w"))
+        out = self._allreduce(out)
+        if self.o_b is not None:
+            out = out + self.o_b
+        return out
+
+    def _mlp(self, x):
+        h = F.linear(x, self._w("fc1_w"), self.fc1_b)
+        if self.spec.gated_mlp:
+            h = DF.gated_activation(h, self.spec.act)
+        else:
+            h = DF.bias_activation(h, None, self.spec.act)
+        out = F.linear(h, self._w("fc2_w"))
+        out = self._allreduce(out)
+        if self.fc2_b is not None:
+            out = out + self.fc2_b
+        return out
+
+    def forward(self, h, residual, meta, cache, rope, alibi):
+        """Pre-norm block. Returns (block_output, residual) where the caller adds them (fused in the next norm)."""
+        if self.spec.parallel_residual:
+            x = h if residual is None else h + residual
+            a_in = self._norm(x, self.ln1_w, self.ln1_b)
+            m_in = a_in if self.spec.shared_parallel_norm else self._norm(x, self.ln2_w, self.ln2_b)
+            out = self._attention(a_in, meta, cache, rope, alibi) + self._mlp(m_in)
+            return out, x
+        if residual is None:
+            normed, residual = self._norm(h, self.ln1_w, self.ln1_b), h
+        else:
+            normed, residual = self._norm(h, self.ln1_w, self.ln1_b, residual)
+        attn = self._attention(normed, meta, cache, rope, alibi)
+        normed, residual = self._norm(attn, self.ln2_w, self.ln2_b, residual)
+        return self._mlp(normed), residual
+
+
+# ------------------------------------------------------------------------------------------------ attention impls
+def _kv_append(k, v, kc, vc, meta):
+    if k.is_cuda and kc.dtype == torch.bfloat16:
+        from ...ops.native import hip_ops
+        hip_ops().kv_append(k, v, kc, vc, meta.block_tables, meta.start_pos)
+        return
+    B, n, Hk, D = k.shape
+    BS = kc.shape[2]
+    for b in range(B):
+        s0 = int(meta.start_pos[b])
+        for j in range(n):
+            t = s0 + j
+            blk = int(meta.block_tables[b, t // BS])
+            kc[blk, :, t % BS] = k[b, j]
+            vc[blk, :, t % BS] = v[b, j]
+
+
+def _alibi_bias(alibi, q_pos, k_len, device):
+    # bias[h, i, j] = slope_h * (j - q_pos_i)
+    kpos = torch.arange(k_len, device=device, dtype=torch.float32)
+    return alibi.to(device)[:, None, None] * (kpos[None, None, :] - q_pos.float()[None, :, None])
+
+
+def _prefill_attention(q, k, v, scale, alibi, window):
+    """q,k,v [B, n, H, D] -> [B, n, Hq, D]; causal."""
+    B, n, Hq, D = q.shape
+    qh, kh, vh = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    if alibi is None and not window:
+        from ...ops.attention import attention
+        return attention(qh, kh, vh, causal=True, softmax_scale=scale).transpose(1, 2)
+    pos = torch.arange(n, device=q.device)
+    mask = torch.zeros(Hq if alibi is not None else 1, n, n, device=q.device, dtype=torch.float32)
+    if alibi is not None:
+        mask = mask + _alibi_bias(alibi, pos, n, q.device)
+    causal = pos[None, :] > pos[:, None]
+    if window:
+        causal = causal | (pos[None, :] <= pos[:, None] - window)
+    mask = mask.masked_fill(causal[None], float("-inf")).to(q.dtype)
+    if kh.shape[1] != Hq:
+        rep = Hq // kh.shape[1]
+        kh, vh = kh.repeat_interleave(rep, 1), vh.repeat_interleave(rep, 1)
+    o = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask[None], scale=scale)
+    return o.transpose(1, 2)
+
+
+def _gather_kv(kc, vc, meta, b, L):
+    BS = kc.shape[2]
+    nblk = (L + BS - 1) // BS
+    ids = meta.block_tables[b, :nblk].long()
+    k = kc[ids].transpose(0, 1).reshape(kc.shape[1], nblk * BS, kc.shape[3])[:, :L]
+    v = vc[ids].transpose(0, 1).reshape(vc.shape[1], nblk * BS, vc.shape[3])[:, :L]
+    return k, v
+
+
+def _cached_attention(q, kc, vc, meta, scale, alibi, window):
+    """General path (chunked prefill / non-bf16 decode): gather each sequence's cache and run SDPA."""
+    B, n, Hq, D = q.shape
+    outs = []
+    seq_lens = meta.seq_lens.tolist()
+    starts = meta.start_pos.tolist()
+    for b in range(B):
+        L = seq_lens[b]
+        k, v = _gather_kv(kc, vc, meta, b, L)
+        rep = Hq // k.shape[0]
+        if rep > 1:
+            k, v = k.repeat_interleave(rep, 0), v.repeat_interleave(rep, 0)
+        qpos = torch.arange(starts[b], starts[b] + n, device=q.device)
+        kpos = torch.arange(L, device=q.device)
+        bad = kpos[None, :] > qpos[:, None]
+        if window:
+            bad = bad | (kpos[None, :] <= qpos[:, None] - window)
+        mask = torch.zeros(Hq if alibi is not None else 1, n, L, device=q.device, dtype=torch.float32)
+        if alibi is not None:
+            mask = mask + _alibi_bias(alibi, qpos, L, q.device)
+        mask = mask.masked_fill(bad[None], float("-inf")).to(q.dtype)
+        o = F.scaled_dot_product_attention(q[b].transpose(0, 1).unsqueeze(0), k.unsqueeze(0), v.unsqueeze(0),
+                                           attn_mask=mask.unsqueeze(0), scale=scale)
+        outs.append(o[0].transpose(0, 1))
+    return torch.stack(outs, 0)
+
+
+def _decode_attention(q, kc, vc, meta, scale, alibi, window):
+    if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128, 256):
+        from ...ops.native import hip_ops
+        return hip_ops().paged_decode(q, kc, vc, meta.block_tables, meta.seq_lens, meta.max_len, scale,
+                                      alibi, window)
+    B, Hq, D = q.shape
+    return _cached_attention(q.view(B, 1, Hq, D), kc, vc, meta, scale, alibi, window).view(B, Hq, D)
+
+
+# ------------------------------------------------------------------------------------------------ model
+class DSInferenceModel(nn.Module):
+
+    def __init__(self, spec: DSModelSpec, tp_group=None, tp_size=1, tp_rank=0, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.spec = spec
+        self.tp_group, self.tp_size, self.tp_rank = tp_group, tp_size, tp_rank
+        self.dtype = dtype
+        self.device = device
+        kw = dict(dtype=dtype, device=device)
+        H = spec.hidden_size
+        self.embed = nn.Parameter(torch.empty(spec.vocab_size, H, **kw), requires_grad=False)
+        self.pos_embed = nn.Parameter(torch.empty(spec.max_positions + spec.learned_pos_offset, H, **kw),
+                                      requires_grad=False) if spec.pos == "learned" else None
+        if spec.embed_norm:
+            self.embed_ln_w = nn.Parameter(torch.ones(H, **kw), requires_grad=False)
+            self.embed_ln_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False)
+        self.layers = nn.ModuleList([DSInferenceLayer(spec, i, tp_group, tp_size, dtype, device)
+                                     for i in range(spec.num_layers)])
+        self.norm_w = nn.Parameter(torch.ones(H, **kw), requires_grad=False)
+        self.norm_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.norm == "ln" else None
+        vloc = (spec.vocab_size + tp_size - 1) // tp_size
+        self.vocab_local = vloc
+        self.lm_head = nn.Parameter(torch.empty(vloc, H, **kw), requires_grad=False)
+        self.lm_head_b = nn.Parameter(torch.zeros(vloc, **kw), requires_grad=False) if spec.lm_head_bias else None
+        if spec.pos in ("rope", "rope_gptj"):
+            cos, sin = reference.rope_tables(max(spec.max_positions, 2048) * 2, spec.rotary_dim, spec.rope_theta,
+                                             device=device)
+            self.register_buffer("rope_cos", cos, persistent=False)
+            self.register_buffer("rope_sin", sin, persistent=False)
+        else:
+            self.rope_cos = self.rope_sin = None
+        if spec.pos == "alibi":
+            slopes = alibi_slopes(spec.num_heads)
+            hq = spec.num_heads // tp_size
+            self.register_buffer("alibi", slopes[tp_rank * hq:(tp_rank + 1) * hq].contiguous().to(device),
+                                 persistent=False)
+        else:
+            self.alibi = None
+        self.cache = None
+
+    # ------------------------------------------------------------------------------------------ cache
+    def allocate_cache(self, num_blocks, block_size=64):
+        from ..kv_cache import BlockedKVCache
+        hk = max(self.spec.num_kv_heads // self.tp_size, 1)
+        self.cache = BlockedKVCache(self.spec.num_layers, num_blocks, hk, block_size, self.spec.head_dim, self.dtype,
+                                    self.device)
+        return self.cache
+
+    # ------------------------------------------------------------------------------------------ forward
+    def _embed(self, input_ids, meta):
+        h = F.embedding(input_ids, self.embed)
+        if self.pos_embed is not None:
+            pos = meta.pos_ids.view(input_ids.shape).long() + self.spec.learned_pos_offset
+            h = h + F.embedding(pos, self.pos_embed)
+        if self.spec.embed_norm:
+            h = DF.layer_norm(h, self.embed_ln_w, self.embed_ln_b, self.spec.norm_eps)
+        return h
+
+    def _logits(self, h):
+        logits = F.linear(h, self.lm_head, self.lm_head_b)
+        if self.tp_size > 1:
+            parts = [torch.empty_like(logits) for _ in range(self.tp_size)]
+            dist.all_gather(parts, logits.contiguous(), group=self.tp_group)
+            logits = torch.cat(parts, dim=-1)
+        return logits[..., :self.spec.vocab_size]
+
+    @torch.no_grad()
+    def forward(self, input_ids, meta: BatchMeta, all_logits=False):
+        """input_ids [B, n] -> logits [B, V] of the last new token (or [B, n, V] with all_logits)."""
+        h = self._embed(input_ids, meta)
+        residual = None
+        rope = (self.rope_cos, self.rope_sin)
+        for layer in self.layers:
+            h, residual = layer(h, residual, meta, self.cache, rope, self.alibi)
+        x = h if residual is None else h + residual
+        if self.spec.final_norm:
+            if self.spec.norm == "rms":
+                x = DF.rms_norm(x, self.norm_w, self.spec.norm_eps)
+            else:
+                x = DF.layer_norm(x, self.norm_w, self.norm_b, self.spec.norm_eps)
+        if not all_logits:
+            x = x[:, -1]
+        return self._logits(x)
+
+    def quantize_weights(self, bits=8, group_size=64):
+        for layer in self.layers:
+            layer.quantize_weights(bits, group_size)

@@ -1,0 +1,237 @@
+// Paged (blocked-KV) decode attention for inference, CDNA4 (gfx950).
+//
+// Parity: reference v1 `softmax_context` over the in-workspace KV cache (`csrc/transformer/inference/csrc/
+// pt_binding.cpp:434-557`, `softmax.cu` attn_softmax_v2 with alibi / causal) and v2 `flash_attn_by_atoms` over the
+// blocked KV cache (`inference/v2/kernels/ragged_ops/blocked_flash`). One kernel serves both engines: a contiguous
+// per-sequence cache is the special case "one block of max_len tokens per sequence".
+//
+// Decode is HBM-bound (every cached K and V byte is read once per token), so the design is flash-decoding:
+//  * grid = (batch, kv_head, split): each workgroup reads ONE kv head's K/V for a contiguous slice of the sequence
+//    once and serves all G = Hq/Hk query heads of that GQA group from it (no K/V re-read per query head);
+//  * the sequence is split so the launch has >= ~2 workgroups per CU even at batch 1 (256 CUs);
+//  * scores for the slice live in LDS; softmax runs on LDS; P·V streams V rows with 16-B loads, 16 lanes per row;
+//  * partial (max, sum, unnormalised acc) per split are merged by a small combine kernel (log-sum-exp).
+// Optional ALiBi slopes (BLOOM) and a sliding window (Mistral) are applied on the fly.
+#include "../include/ds_hip.h"
+
+namespace {
+
+constexpr int THREADS = 256;
+constexpr int MAXG = 8;          // query heads per kv head handled per workgroup (GQA group)
+constexpr int MAX_CHUNK = 1024;  // keys per split (LDS: MAXG * MAX_CHUNK * 4 B = 32 KiB)
+
+template <int D>
+__global__ void __launch_bounds__(THREADS) paged_decode_kernel(
+    const bf16* __restrict__ q,          // [B, Hq, D]
+    const bf16* __restrict__ kc,         // [NB, Hk, BS, D]
+    const bf16* __restrict__ vc,         // [NB, Hk, BS, D]
+    const int* __restrict__ block_table, // [B, max_blocks]
+    const int* __restrict__ seq_lens,    // [B]
+    const float* __restrict__ alibi,     // [Hq] or null
+    float* __restrict__ part_acc,        // [B, Hq, S, D]  (only if S > 1)
+    float* __restrict__ part_ml,         // [B, Hq, S, 2]
+    bf16* __restrict__ out,              // [B, Hq, D]  (written directly when S == 1)
+    int Hq, int Hk, int BS, int max_blocks, int chunk, float scale, int window) {
+  static_assert(D % 64 == 0 && D <= 256, "head dim");
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // scores [G][chunk] + reduction scratch
+  const int b = blockIdx.x, kh = blockIdx.y, split = blockIdx.z, S = gridDim.z;
+  const int G = Hq / Hk;
+  const int T = seq_lens[b];
+  const int t0 = split * chunk;
+  const int t1 = min(T, t0 + chunk);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tlo = window > 0 ? max(0, T - window) : 0;
+  float* scores = sm;                       // [G][chunk]
+  float* red = sm + MAXG * MAX_CHUNK;       // [THREADS/64 * MAXG * 2]
+
+  // ---- q of the G heads of this GQA group; LPR = D/8 lanes cover one row, 8 elements each
+  constexpr int LPR = D / 8;                // lanes per key row (16 for D=128)
+  constexpr int RPW = 64 / LPR;             // rows per wave instruction
+  const int sub = lane / LPR, li = lane % LPR;
+  float qv[MAXG][8];
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g) {
+    if (g < G) {
+      Vec8<bf16>::load(q + ((int64_t)b * Hq + kh * G + g) * D + li * 8, qv[g]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qv[g][j] *= scale;
+    }
+  }
+  // ---- phase 1: scores for keys of this split
+  const int* bt = block_table + (int64_t)b * max_blocks;
+  for (int t = t0 + wid * RPW + sub; t < t1; t += (THREADS / 64) * RPW) {
+    const int blk = bt[t / BS], off = t % BS;
+    float kv[8];
+    Vec8<bf16>::load(kc + (((int64_t)blk * Hk + kh) * BS + off) * D + li * 8, kv);
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < G) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s = fmaf(qv[g][j], kv[j], s);
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (li == 0) {
+          if (alibi) s += alibi[kh * G + g] * (float)(t - (T - 1));
+          if (t < tlo) s = -INFINITY;
+          scores[g * MAX_CHUNK + (t - t0)] = s;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: per-head max and sum over the split (one wave per head group, strided)
+  const int n = t1 - t0;
+  for (int g = wid; g < G; g += THREADS / 64) {
+    float m = -INFINITY;
+    for (int i = lane; i < n; i += 64) m = fmaxf(m, scores[g * MAX_CHUNK + i]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int i = lane; i < n; i += 64) {
+      const float p = (m == -INFINITY) ? 0.f : __expf(scores[g * MAX_CHUNK + i] - m);
+      scores[g * MAX_CHUNK + i] = p;
+      l += p;
+    }
+    l = wave_sum(l);
+    if (lane == 0) {
+      red[g * 2] = m;
+      red[g * 2 + 1] = l;
+    }
+  }
+  __syncthreads();
+  // ---- phase 3: acc[g][d] = sum_t p[g][t] * v[t][d]; LPR lanes per V row, THREADS/LPR rows in flight
+  constexpr int ROWS = THREADS / LPR;
+  const int r = tid / LPR, c = tid % LPR;
+  float acc[MAXG][8];
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  for (int t = t0 + r; t < t1; t += ROWS) {
+    const int blk = bt[t / BS], off = t % BS;
+    float vv[8];
+    Vec8<bf16>::load(vc + (((int64_t)blk * Hk + kh) * BS + off) * D + c * 8, vv);
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < G) {
+        const float p = scores[g * MAX_CHUNK + (t - t0)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(p, vv[j], acc[g][j]);
+      }
+    }
+  }
+  __syncthreads();  // scores are dead: reuse their LDS as a [ROWS][D] buffer, one query head at a time
+  float* rb = sm;
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g) {
+    if (g >= G) break;  // block-uniform
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rb[r * D + c * 8 + j] = acc[g][j];
+    __syncthreads();
+    for (int idx = tid; idx < D; idx += THREADS) {
+      float s = 0.f;
+      for (int rr = 0; rr < ROWS; ++rr) s += rb[rr * D + idx];
+      const int hq = kh * G + g;
+      const float m = red[g * 2], l = red[g * 2 + 1];
+      if (S == 1) {
+        out[((int64_t)b * Hq + hq) * D + idx] = (bf16)(l > 0.f ? s / l : 0.f);
+      } else {
+        part_acc[(((int64_t)b * Hq + hq) * S + split) * D + idx] = s;
+        if (idx == 0) {
+          part_ml[(((int64_t)b * Hq + hq) * S + split) * 2] = m;
+          part_ml[(((int64_t)b * Hq + hq) * S + split) * 2 + 1] = l;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(D) combine_kernel(const float* __restrict__ part_acc,
+                                                    const float* __restrict__ part_ml, bf16* __restrict__ out, int S) {
+  const int bh = blockIdx.x, d = threadIdx.x;
+  float M = -INFINITY;
+  for (int s = 0; s < S; ++s) M = fmaxf(M, part_ml[((int64_t)bh * S + s) * 2]);
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const float m = part_ml[((int64_t)bh * S + s) * 2], l = part_ml[((int64_t)bh * S + s) * 2 + 1];
+    if (m == -INFINITY) continue;
+    const float w = __expf(m - M);
+    num = fmaf(w, part_acc[((int64_t)bh * S + s) * D + d], num);
+    den = fmaf(w, l, den);
+  }
+  out[(int64_t)bh * D + d] = (bf16)(den > 0.f ? num / den : 0.f);
+}
+
+// Write new K/V rows into the paged cache: k,v [B, n_new, Hk, D] token-major; positions start at seq_lens_before[b].
+__global__ void __launch_bounds__(256) kv_append_kernel(const bf16* __restrict__ k, const bf16* __restrict__ v,
+                                                        bf16* __restrict__ kc, bf16* __restrict__ vc,
+                                                        const int* __restrict__ block_table,
+                                                        const int* __restrict__ start_pos, int B, int n_new, int Hk,
+                                                        int D, int BS, int max_blocks) {
+  const int64_t vec_per_row = D / 8;
+  const int64_t total = (int64_t)B * n_new * Hk * vec_per_row;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cvec = (int)(i % vec_per_row);
+    int64_t r = i / vec_per_row;
+    const int h = (int)(r % Hk);
+    r /= Hk;
+    const int j = (int)(r % n_new), b = (int)(r / n_new);
+    const int t = start_pos[b] + j;
+    const int blk = block_table[(int64_t)b * max_blocks + t / BS], off = t % BS;
+    const int64_t src = (((int64_t)b * n_new + j) * Hk + h) * D + cvec * 8;
+    const int64_t dst = (((int64_t)blk * Hk + h) * BS + off) * D + cvec * 8;
+    *reinterpret_cast<bf16x8*>(kc + dst) = *reinterpret_cast<const bf16x8*>(k + src);
+    *reinterpret_cast<bf16x8*>(vc + dst) = *reinterpret_cast<const bf16x8*>(v + src);
+  }
+}
+
+}  // namespace
+
+extern "C" int ds_paged_decode_splits(int B, int Hk, int max_len) {
+  // enough workgroups to cover the chip ~2x, splits of >= 64 keys, <= MAX_CHUNK keys per split
+  const int want = (512 + B * Hk - 1) / (B * Hk);
+  int chunk = (max_len + want - 1) / want;
+  chunk = ((chunk + 63) / 64) * 64;
+  if (chunk < 64) chunk = 64;
+  if (chunk > MAX_CHUNK) chunk = MAX_CHUNK;
+  return (max_len + chunk - 1) / chunk;
+}
+
+extern "C" int ds_paged_decode(const void* q, const void* kc, const void* vc, const int* block_table,
+                               const int* seq_lens, const float* alibi, float* part_acc, float* part_ml, void* out,
+                               int B, int Hq, int Hk, int D, int BS, int max_blocks, int max_len, int splits,
+                               float scale, int window, hipStream_t s) {
+  if (Hq % Hk || Hq / Hk > MAXG) return (int)hipErrorInvalidValue;
+  const int chunk = ((max_len + splits - 1) / splits + 63) / 64 * 64;
+  if (chunk > MAX_CHUNK) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(MAXG * MAX_CHUNK + 64) * sizeof(float);
+  dim3 grid(B, Hk, splits);
+#define LAUNCH(DD)                                                                                                  \
+  hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, dim3(THREADS), lds, s, (const bf16*)q, (const bf16*)kc,       \
+                     (const bf16*)vc, block_table, seq_lens, alibi, part_acc, part_ml, (bf16*)out, Hq, Hk, BS,       \
+                     max_blocks, chunk, scale, window);                                                             \
+  DS_CHECK_LAUNCH();                                                                                                \
+  if (splits > 1) {                                                                                                 \
+    hipLaunchKernelGGL((combine_kernel<DD>), dim3(B * Hq), dim3(DD), 0, s, part_acc, part_ml, (bf16*)out, splits);  \
+    DS_CHECK_LAUNCH();                                                                                              \
+  }
+  if (D == 64) { LAUNCH(64) }
+  else if (D == 128) { LAUNCH(128) }
+  else if (D == 256) { LAUNCH(256) }
+  else return (int)hipErrorInvalidValue;
+#undef LAUNCH
+  return 0;
+}
+
+extern "C" int ds_kv_append(const void* k, const void* v, void* kc, void* vc, const int* block_table,
+                            const int* start_pos, int B, int n_new, int Hk, int D, int BS, int max_blocks,
+                            hipStream_t s) {
+  if (D % 8) return (int)hipErrorInvalidValue;
+  const int grid = ds_grid_for((int64_t)B * n_new * Hk * (D / 8), 256);
+  hipLaunchKernelGGL(kv_append_kernel, dim3(grid), dim3(256), 0, s, (const bf16*)k, (const bf16*)v, (bf16*)kc,
+                     (bf16*)vc, block_table, start_pos, B, n_new, Hk, D, BS, max_blocks);
+  DS_CHECK_LAUNCH();
+  return 0;
+}

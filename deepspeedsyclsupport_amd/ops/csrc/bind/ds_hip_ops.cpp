@@ -347,7 +347,11 @@ Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, OptT dloss, double dlo
 
 }  // namespace
 
+// other binding translation units of this extension
+void register_inference_ops(pybind11::module& m);  // bind/infer_bind.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  register_inference_ops(m);
   m.doc() = "deepspeedsyclsupport_amd gfx950 kernels";
   m.def("adam_flat", &adam_flat);
   m.def("adam_multi", &adam_multi);

@@ -38,8 +38,10 @@ EXTENSIONS = {
             "act/act_kernels.hip",
             "rope/rope_kernels.hip",
             "xent/xent_kernels.hip",
+            "attn/decode_attn.hip",
+            "quant/quant_kernels.hip",
         ],
-        "binding": "bind/ds_hip_ops.cpp",
+        "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp"],
     },
     # host ops: CPU Adam/Adagrad/Lion (ZeRO-Offload, Twin-Flow), async tensor I/O (ZeRO-Infinity), shm all-reduce
     "ds_cpu_ops": {
@@ -119,10 +121,11 @@ def _write_ninja(names):
                 obj = os.path.join(BUILD_DIR, name, src.replace("/", "_") + ".o")
                 lines.append(f"build {obj}: hip {os.path.join(CSRC, src)}")
                 objs.append(obj)
-            bobj = os.path.join(BUILD_DIR, name, "bind.o")
-            lines.append(f"build {bobj}: cxx {os.path.join(CSRC, spec['binding'])}")
-            lines.append(f"  extra = -DTORCH_EXTENSION_NAME={name} -I{CSRC}/include")
-            objs.append(bobj)
+            for bsrc in spec["bindings"]:
+                bobj = os.path.join(BUILD_DIR, name, bsrc.replace("/", "_") + ".o")
+                lines.append(f"build {bobj}: cxx {os.path.join(CSRC, bsrc)}")
+                lines.append(f"  extra = -DTORCH_EXTENSION_NAME={name} -I{CSRC}/include")
+                objs.append(bobj)
             libs_ = "-lamdhip64 -lc10 -ltorch -ltorch_cpu -ltorch_python -lc10_hip -ltorch_hip"
         else:
             for src in spec["sources"]:
