@@ -1,0 +1,294 @@
+"""Inference engine (reference `inference/engine.py:42-620`: TP group creation, kernel injection / AutoTP, dtype
+conversion, CUDA-graph capture, generate wrapper, checkpoint loading).
+
+MI355X design:
+* Kernel injection replaces the whole HF decoder with `DSInferenceModel` (paged KV cache, HIP decode attention,
+  fused norm/act kernels, hipBLASLt GEMMs) instead of patching modules one by one; AutoTP (no injection) shards the
+  HF model's own Linear layers (`module_inject.auto_tp`).
+* Decode steps are captured once per batch size into a HIP graph (`enable_cuda_graph`) over static input/metadata
+  buffers; each step is then one graph launch (the per-layer launch overhead dominates small-batch decode).
+* Tensor parallel groups are consecutive ranks (one node's GPUs over xGMI); two all-reduces per layer.
+"""
+import time
+
+import torch
+
+from .. import comm as dist
+from ..accelerator import get_accelerator
+from ..utils.logging import log_dist
+from .config import DeepSpeedInferenceConfig
+from .model_implementations import convert
+from .model_implementations.transformer import BatchMeta, DSInferenceModel
+
+
+class GenerationOutput:
+
+    def __init__(self, logits):
+        self.logits = logits
+
+    def __getitem__(self, i):
+        return (self.logits, )[i]
+
+
+class InferenceEngine(torch.nn.Module):
+    inference_mp_group = None
+    inference_ep_group = None
+
+    def __init__(self, model, config: DeepSpeedInferenceConfig):
+        super().__init__()
+        self._config = config
+        self.dtype = config.dtype
+        self.injection_dict = config.injection_policy
+        self.mp_group = config.tensor_parallel.tp_group
+        self.mpu = config.tensor_parallel.mpu
+        self.quantize_merge_count = 1
+        self.quantization_scales = None
+        self.model_profile_enabled = False
+        self._model_times = []
+        self.cuda_graph_created = False
+        self._graphs = {}
+        acc = get_accelerator()
+        self.device = torch.device(acc.device_name(acc.current_device())) if acc.device_name() != "cpu" \
+            else torch.device("cpu")
+
+        tp = config.tensor_parallel.tp_size
+        if tp > 1 or (dist.is_initialized() and dist.get_world_size() > 1):
+            if not dist.is_initialized():
+                dist.init_distributed(dist_backend=acc.communication_backend_name())
+        self.tp_size = tp if tp > 1 else 1
+        if self.tp_size > 1:
+            self._create_model_parallel_group(config)
+            self.tp_rank = dist.get_rank(self.mp_group)
+        else:
+            self.tp_rank = 0
+
+        if config.checkpoint is not None and not isinstance(model, torch.nn.Module):
+            raise ValueError("init_inference expects an nn.Module (meta-tensor checkpoint loading: pass the model)")
+
+        self.injected = False
+        if (config.replace_with_kernel_inject or _is_native(model)) and convert.supported(model):
+            self.module = convert.from_model(model, self.mp_group, self.tp_size, self.tp_rank, self.dtype, self.device,
+                                             max_positions=config.max_out_tokens)
+            self.injected = True
+            if config.quant.enabled and config.quant.weight.enabled:
+                self.module.quantize_weights(config.quant.weight.num_bits, config.quant.weight.group_size)
+            del model
+        else:
+            if self.tp_size > 1:
+                from ..module_inject.auto_tp import AutoTP
+                AutoTP(model, self.mp_group, self.tp_size, self.tp_rank).apply()
+            self.module = model.to(self.device)
+            if self.dtype in (torch.float16, torch.bfloat16, torch.float32):
+                self.module = self.module.to(self.dtype)
+        self.module.eval()
+        log_dist(f"InferenceEngine: injected={self.injected} tp={self.tp_size} dtype={self.dtype}", ranks=[0])
+
+    # ------------------------------------------------------------------------------------------ groups
+    def _create_model_parallel_group(self, config):
+        if self.mpu is not None:
+            self.mp_group = self.mpu.get_model_parallel_group()
+        elif self.mp_group is None:
+            world, rank, tp = dist.get_world_size(), dist.get_rank(), self.tp_size
+            assert world % tp == 0, f"world {world} not divisible by tp {tp}"
+            for start in range(0, world, tp):
+                ranks = list(range(start, start + tp))
+                g = dist.new_group(ranks)
+                if rank in ranks:
+                    self.mp_group = g
+        InferenceEngine.inference_mp_group = self.mp_group
+
+    # ------------------------------------------------------------------------------------------ profiling
+    def profile_model_time(self, use_cuda_events=True):
+        self.model_profile_enabled = True
+
+    def model_times(self):
+        out, self._model_times = self._model_times, []
+        return out
+
+    # ------------------------------------------------------------------------------------------ helpers
+    def _cache_for(self, total_tokens_per_seq, batch):
+        bs = self._config.kv_block_size
+        per_seq = (total_tokens_per_seq + bs - 1) // bs
+        need = per_seq * batch
+        c = self.module.cache
+        if c is None or c.num_blocks < need or c.block_size != bs:
+            self.module.allocate_cache(max(need, per_seq * min(self._config.max_batch_size, batch * 2)), bs)
+            self._graphs.clear()
+        return per_seq
+
+    def _meta(self, block_tables, starts, n_new, max_len):
+        dev = self.device
+        st = torch.tensor(starts, dtype=torch.int32, device=dev)
+        pos = (st[:, None] + torch.arange(n_new, dtype=torch.int32, device=dev)[None, :]).reshape(-1)
+        return BatchMeta(block_tables=block_tables, start_pos=st, seq_lens=st + n_new, pos_ids=pos.contiguous(),
+                         n_new=n_new, max_len=max_len, prefill_from_zero=all(s == 0 for s in starts))
+
+    @staticmethod
+    def _unpad(input_ids, attention_mask):
+        rows = []
+        for b in range(input_ids.shape[0]):
+            ids = input_ids[b]
+            if attention_mask is not None:
+                ids = ids[attention_mask[b].bool()]
+            rows.append(ids)
+        return rows
+
+    # ------------------------------------------------------------------------------------------ forward
+    def forward(self, *inputs, **kwargs):
+        start = time.time() if self.model_profile_enabled else None
+        if not self.injected:
+            out = self.module(*inputs, **kwargs)
+        else:
+            input_ids = inputs[0] if inputs else kwargs["input_ids"]
+            out = GenerationOutput(self._full_logits(input_ids.to(self.device), kwargs.get("attention_mask")))
+        if start is not None:
+            get_accelerator().synchronize()
+            self._model_times.append(time.time() - start)
+        return out
+
+    @torch.no_grad()
+    def _full_logits(self, input_ids, attention_mask=None):
+        B, S = input_ids.shape
+        per_seq = self._cache_for(S, B)
+        alloc = self.module.cache.allocator
+        blocks = alloc.allocate(per_seq * B)
+        try:
+            bt = torch.tensor(blocks, dtype=torch.int32, device=self.device).view(B, per_seq)
+            if attention_mask is None or bool(attention_mask.all()):
+                meta = self._meta(bt, [0] * B, S, S)
+                return self.module(input_ids, meta, all_logits=True)
+            V = self.module.spec.vocab_size
+            out = torch.zeros(B, S, V, dtype=self.dtype, device=self.device)
+            for b, ids in enumerate(self._unpad(input_ids, attention_mask)):
+                meta = self._meta(bt[b:b + 1], [0], ids.numel(), ids.numel())
+                lg = self.module(ids[None], meta, all_logits=True)[0]
+                out[b, attention_mask[b].bool()] = lg
+            return out
+        finally:
+            alloc.free(blocks)
+
+    # ------------------------------------------------------------------------------------------ generate
+    def _sample(self, logits, do_sample, temperature, top_k, top_p, generator):
+        if not do_sample:
+            return logits.argmax(-1)
+        logits = logits.float() / max(temperature, 1e-5)
+        if top_k and top_k > 0:
+            kth = torch.topk(logits, min(top_k, logits.shape[-1]), dim=-1).values[..., -1:]
+            logits = logits.masked_fill(logits < kth, float("-inf"))
+        if top_p is not None and top_p < 1.0:
+            srt, idx = torch.sort(logits, descending=True, dim=-1)
+            cum = srt.softmax(-1).cumsum(-1)
+            drop = cum - srt.softmax(-1) > top_p
+            srt = srt.masked_fill(drop, float("-inf"))
+            logits = torch.full_like(logits, float("-inf")).scatter(-1, idx, srt)
+        probs = logits.softmax(-1)
+        return torch.multinomial(probs, 1, generator=generator).squeeze(-1)
+
+    def _decode_step(self, ids, bt, lens, max_len):
+        """One decode step for every sequence (ids [B, 1]); uses a captured HIP graph when enabled."""
+        B = ids.shape[0]
+        if not (self._config.enable_cuda_graph and self.device.type == "cuda"):
+            meta = self._meta(bt, lens, 1, max_len)
+            return self.module(ids, meta)
+        key = (B, bt.shape[1])
+        g = self._graphs.get(key)
+        st = torch.tensor(lens, dtype=torch.int32, device=self.device)
+        if g is None:
+            static = dict(ids=ids.clone(), bt=bt.clone(), st=st.clone())
+            cap = bt.shape[1] * self.module.cache.block_size
+
+            def run():
+                meta = BatchMeta(block_tables=static["bt"], start_pos=static["st"], seq_lens=static["st"] + 1,
+                                 pos_ids=static["st"], n_new=1, max_len=cap, prefill_from_zero=False)
+                return self.module(static["ids"], meta)
+
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                run()  # warm up allocations / library handles outside capture
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static["out"] = run()
+            g = self._graphs[key] = (graph, static)
+            self.cuda_graph_created = True
+        graph, static = g
+        static["ids"].copy_(ids)
+        static["bt"].copy_(bt)
+        static["st"].copy_(st)
+        graph.replay()
+        return static["out"]
+
+    @torch.no_grad()
+    def generate(self, input_ids=None, attention_mask=None, max_new_tokens=None, max_length=None, do_sample=False,
+                 temperature=1.0, top_k=0, top_p=1.0, eos_token_id=None, pad_token_id=None, seed=None, **kwargs):
+        if not self.injected:
+            return self.module.generate(input_ids=input_ids, attention_mask=attention_mask,
+                                        max_new_tokens=max_new_tokens, max_length=max_length, do_sample=do_sample,
+                                        **kwargs)
+        input_ids = input_ids.to(self.device)
+        B, S = input_ids.shape
+        if max_new_tokens is None:
+            max_new_tokens = (max_length - S) if max_length else self._config.max_out_tokens - S
+        max_new_tokens = max(int(max_new_tokens), 0)
+        if attention_mask is not None:
+            attention_mask = attention_mask.to(self.device)
+        rows = self._unpad(input_ids, attention_mask)
+        lens = [int(r.numel()) for r in rows]
+        total = max(lens) + max_new_tokens
+        per_seq = self._cache_for(total, B)
+        alloc = self.module.cache.allocator
+        blocks = alloc.allocate(per_seq * B)
+        gen = None
+        if do_sample:
+            gen = torch.Generator(device=self.device)
+            gen.manual_seed(seed if seed is not None else int(torch.initial_seed()) % (2**31))
+        eos = set([eos_token_id] if isinstance(eos_token_id, int) else (eos_token_id or []))
+        pad = pad_token_id if pad_token_id is not None else (next(iter(eos)) if eos else 0)
+        try:
+            bt = torch.tensor(blocks, dtype=torch.int32, device=self.device).view(B, per_seq)
+            # prefill (one batched launch when all prompts have the same length)
+            if len(set(lens)) == 1:
+                meta = self._meta(bt, [0] * B, lens[0], lens[0])
+                logits = self.module(torch.stack(rows), meta)
+            else:
+                logits = torch.cat([
+                    self.module(rows[b][None], self._meta(bt[b:b + 1], [0], lens[b], lens[b]))
+                    for b in range(B)
+                ])
+            out_tokens = []
+            done = torch.zeros(B, dtype=torch.bool, device=self.device)
+            eos_t = torch.tensor(sorted(eos), device=self.device) if eos else None
+            cur = list(lens)
+            max_len = per_seq * self.module.cache.block_size
+            for step in range(max_new_tokens):
+                nxt = self._sample(logits, do_sample, temperature, top_k, top_p, gen)
+                nxt = torch.where(done, torch.full_like(nxt, pad), nxt)
+                out_tokens.append(nxt)
+                if eos_t is not None:
+                    done = done | torch.isin(nxt, eos_t)
+                    if (step & 15) == 15 and bool(done.all()):
+                        break
+                if step == max_new_tokens - 1:
+                    break
+                logits = self._decode_step(nxt[:, None].contiguous(), bt, cur, max_len)
+                cur = [c + 1 for c in cur]
+        finally:
+            alloc.free(blocks)
+        if not out_tokens:
+            return input_ids
+        gen_ids = torch.stack(out_tokens, 1).to(input_ids.dtype)
+        return torch.cat([input_ids, gen_ids], 1)
+
+    def _generate(self, *args, **kwargs):
+        return self.generate(*args, **kwargs)
+
+    def destroy(self):
+        self._graphs.clear()
+        if self.injected:
+            self.module.cache = None
+
+
+def _is_native(model):
+    from ..models.llama import LlamaForCausalLM
+    return isinstance(model, LlamaForCausalLM)

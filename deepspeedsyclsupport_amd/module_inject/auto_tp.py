@@ -1,0 +1,128 @@
+"""Automatic tensor parallelism for arbitrary HF models (reference `module_inject/auto_tp.py:186-500`,
+`fusedqkv_utils.py`, `tp_shard.py`).
+
+Walks the model, classifies each Linear / HF Conv1D inside a repeated block as
+  * row-parallel ("all-reduce") if its name marks an output projection (o_proj, out_proj, down_proj, dense_4h_to_h,
+    c_proj, fc2, fc_out, w2, wo, attention `dense`) -> `LinearAllreduce` with a column slice of W,
+  * column-parallel otherwise -> `LinearLayer` with a row slice (fused QKV weights are sliced per q/k/v part or per
+    head for interleaved layouts, so every rank keeps whole heads),
+and divides the head-count attributes of attention modules so HF reshapes see the local head count.
+Embeddings and the LM head stay replicated (vocab GEMM is cheap relative to 288 GB HBM).
+"""
+import re
+
+import torch
+import torch.nn as nn
+
+from .layers import LinearAllreduce, LinearLayer
+
+ROW_PARALLEL = ("o_proj", "out_proj", "down_proj", "dense_4h_to_h", "c_proj", "fc2", "fc_out", "w2", "wo",
+                "proj_out")
+ATTN_DENSE = re.compile(r"(attention|attn|self_attention)\.dense$")
+FUSED_BLOCKS = ("c_attn", "qkv_proj", "Wqkv", "qkv")          # [q | k | v] stacked along the output dim
+FUSED_INTERLEAVED = ("query_key_value", )                   # [heads, 3, D] interleaved (BLOOM / GPT-NeoX)
+FUSED_GATE_UP = ("gate_up_proj", )
+HEAD_ATTRS = ("num_heads", "num_attention_heads", "num_key_value_heads", "num_kv_heads", "n_head", "n_heads")
+WIDTH_ATTRS = ("split_size", "all_head_size", "embed_dim", "hidden_size_per_partition", "inner_dim")
+
+
+def _is_conv1d(m):
+    return type(m).__name__ == "Conv1D" and hasattr(m, "nf")
+
+
+def _linear_weight(m):
+    """Return W as [out, in] regardless of Linear vs Conv1D."""
+    return m.weight.data.t() if _is_conv1d(m) else m.weight.data
+
+
+def _slice_rows(w, r, tp):
+    n = w.shape[0] // tp
+    return w[r * n:(r + 1) * n].contiguous()
+
+
+class AutoTP:
+
+    def __init__(self, model, mp_group, tp_size, tp_rank, kv_heads=None):
+        self.model = model
+        self.mp_group = mp_group
+        self.tp = tp_size
+        self.rank = tp_rank
+        cfg = getattr(model, "config", None)
+        self.num_heads = getattr(cfg, "num_attention_heads", None) or getattr(cfg, "n_head", None)
+        self.kv_heads = kv_heads or getattr(cfg, "num_key_value_heads", None) or self.num_heads
+        self.replaced = []
+
+    # ------------------------------------------------------------------------------------------ policy
+    @staticmethod
+    def is_row_parallel(name):
+        leaf = name.split(".")[-1]
+        return leaf in ROW_PARALLEL or bool(ATTN_DENSE.search(name)) or name.endswith("output.dense")
+
+    @staticmethod
+    def in_block(name):
+        return bool(re.search(r"\.(\d+)\.", "." + name + "."))
+
+    # ------------------------------------------------------------------------------------------ slicing
+    def _column(self, name, m):
+        w = _linear_weight(m)
+        b = m.bias.data if m.bias is not None else None
+        leaf = name.split(".")[-1]
+        r, tp = self.rank, self.tp
+        if leaf in FUSED_BLOCKS and self.num_heads:
+            D = w.shape[1] // self.num_heads
+            sizes = [self.num_heads * D, self.kv_heads * D, self.kv_heads * D]
+            if sum(sizes) != w.shape[0]:
+                sizes = [w.shape[0] // 3] * 3
+            parts = w.split(sizes, 0)
+            w = torch.cat([_slice_rows(p, r, tp) for p in parts], 0)
+            if b is not None:
+                b = torch.cat([_slice_rows(p, r, tp) for p in b.split(sizes, 0)], 0)
+        elif leaf in FUSED_GATE_UP:
+            parts = w.chunk(2, 0)
+            w = torch.cat([_slice_rows(p, r, tp) for p in parts], 0)
+            if b is not None:
+                b = torch.cat([_slice_rows(p, r, tp) for p in b.chunk(2, 0)], 0)
+        else:  # plain or head-interleaved fused qkv: contiguous row slice keeps whole heads
+            w = _slice_rows(w, r, tp)
+            if b is not None:
+                b = _slice_rows(b, r, tp)
+        return LinearLayer(weight=nn.Parameter(w.contiguous(), requires_grad=False),
+                           bias=None if b is None else nn.Parameter(b.contiguous(), requires_grad=False))
+
+    def _row(self, name, m):
+        w = _linear_weight(m)
+        n = w.shape[1] // self.tp
+        w = w[:, self.rank * n:(self.rank + 1) * n].contiguous()
+        b = m.bias.data if m.bias is not None else None
+        return LinearAllreduce(nn.Parameter(w, requires_grad=False),
+                               None if b is None else nn.Parameter(b.clone(), requires_grad=False), self.mp_group)
+
+    # ------------------------------------------------------------------------------------------ apply
+    def apply(self):
+        if self.tp <= 1:
+            return self.model
+        targets = []
+        for name, m in self.model.named_modules():
+            if (isinstance(m, nn.Linear) or _is_conv1d(m)) and self.in_block(name):
+                targets.append((name, m))
+        for name, m in targets:
+            new = self._row(name, m) if self.is_row_parallel(name) else self._column(name, m)
+            parent_name, _, leaf = name.rpartition(".")
+            parent = self.model.get_submodule(parent_name) if parent_name else self.model
+            setattr(parent, leaf, new)
+            self.replaced.append((name, type(new).__name__))
+        self._fix_attrs()
+        return self.model
+
+    def _fix_attrs(self):
+        for name, m in self.model.named_modules():
+            if not re.search(r"attn|attention", name.split(".")[-1] if name else "", re.I):
+                continue
+            for a in HEAD_ATTRS:
+                v = getattr(m, a, None)
+                if isinstance(v, int) and v >= self.tp and v % self.tp == 0:
+                    setattr(m, a, v // self.tp)
+            for a in WIDTH_ATTRS:
+                v = getattr(m, a, None)
+                if isinstance(v, int) and v % self.tp == 0:
+                    setattr(m, a, v // self.tp)

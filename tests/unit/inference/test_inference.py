@@ -1,0 +1,194 @@
+"""Kernel-injected inference (reference `tests/unit/inference/test_inference.py`: per-model output parity of
+`init_inference` against the HF pipeline, TP via `mp_size`, int8 quantisation, CUDA graphs).
+
+HF reference models are tiny random-init instances built from their configs (no network / checkpoints). CPU runs
+use fp32 and demand near-bitwise parity; TP=2 runs use gloo ranks; GPU tests check the bf16 HIP path (paged decode,
+fused kernels, HIP-graph decode) against the fp32 HF model.
+"""
+import pytest
+import torch
+
+from ..common import run_distributed
+
+transformers = pytest.importorskip("transformers")
+V = 256
+
+
+def tiny(kind):
+    T = transformers
+    torch.manual_seed(0)
+    if kind == "llama":
+        c = T.LlamaConfig(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                          num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
+        return T.LlamaForCausalLM(c)
+    if kind == "mistral":
+        c = T.MistralConfig(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                            num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128,
+                            sliding_window=8)
+        return T.MistralForCausalLM(c)
+    if kind == "qwen2":
+        c = T.Qwen2Config(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                          num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
+        return T.Qwen2ForCausalLM(c)
+    if kind == "gpt2":
+        return T.GPT2LMHeadModel(T.GPT2Config(vocab_size=V, n_embd=64, n_layer=2, n_head=4, n_positions=128,
+                                              bos_token_id=0, eos_token_id=1))
+    if kind == "bloom":
+        return T.BloomForCausalLM(T.BloomConfig(vocab_size=V, hidden_size=64, n_layer=2, n_head=4))
+    if kind == "opt":
+        return T.OPTForCausalLM(T.OPTConfig(vocab_size=V, hidden_size=64, num_hidden_layers=2, ffn_dim=128,
+                                            num_attention_heads=4, max_position_embeddings=128,
+                                            word_embed_proj_dim=64))
+    if kind == "gpt_neox":
+        return T.GPTNeoXForCausalLM(T.GPTNeoXConfig(vocab_size=V, hidden_size=64, num_hidden_layers=2,
+                                                    num_attention_heads=4, intermediate_size=128,
+                                                    max_position_embeddings=128))
+    if kind == "gptj":
+        return T.GPTJForCausalLM(T.GPTJConfig(vocab_size=V, n_embd=64, n_layer=2, n_head=4, rotary_dim=8,
+                                              n_positions=128, bos_token_id=0, eos_token_id=1))
+    raise ValueError(kind)
+
+
+ARCHS = ["llama", "mistral", "qwen2", "gpt2", "bloom", "opt", "gpt_neox", "gptj"]
+
+
+def _ids(B=2, S=12, seed=1):
+    return torch.randint(2, V, (B, S), generator=torch.Generator().manual_seed(seed))
+
+
+@pytest.mark.parametrize("kind", ARCHS)
+def test_injected_parity_cpu(kind):
+    import deepspeedsyclsupport_amd as ds
+    m = tiny(kind).eval()
+    ids = _ids()
+    with torch.no_grad():
+        ref = m(ids).logits
+    eng = ds.init_inference(m, dtype=torch.float32, replace_with_kernel_inject=True)
+    assert eng.injected
+    out = eng(ids).logits
+    assert (out - ref).abs().max().item() < 1e-4
+    g_ref = m.generate(ids, max_new_tokens=6, do_sample=False, pad_token_id=0)
+    assert torch.equal(eng.generate(ids, max_new_tokens=6), g_ref)
+
+
+def test_padded_batch_and_sampling():
+    import deepspeedsyclsupport_amd as ds
+    m = tiny("llama").eval()
+    ids = _ids()
+    mask = torch.ones_like(ids)
+    ids[0, :4], mask[0, :4] = 0, 0
+    eng = ds.init_inference(m, dtype=torch.float32, replace_with_kernel_inject=True)
+    g = eng.generate(ids, attention_mask=mask, max_new_tokens=5)
+    assert torch.equal(g[0, -5:], m.generate(ids[0:1, 4:], max_new_tokens=5, do_sample=False)[0, -5:])
+    assert torch.equal(g[1], m.generate(ids[1:2], max_new_tokens=5, do_sample=False)[0])
+    s1 = eng.generate(ids[1:], max_new_tokens=5, do_sample=True, top_k=10, top_p=0.9, temperature=0.8, seed=3)
+    s2 = eng.generate(ids[1:], max_new_tokens=5, do_sample=True, top_k=10, top_p=0.9, temperature=0.8, seed=3)
+    assert torch.equal(s1, s2) and s1.shape == (1, 17)
+
+
+def test_eos_stops_and_pads():
+    import deepspeedsyclsupport_amd as ds
+    m = tiny("llama").eval()
+    ids = _ids(B=1)
+    eng = ds.init_inference(m, dtype=torch.float32, replace_with_kernel_inject=True)
+    g = eng.generate(ids, max_new_tokens=8)
+    eos = int(g[0, 14])  # force the third generated token to be "EOS"
+    g2 = eng.generate(ids, max_new_tokens=8, eos_token_id=eos, pad_token_id=0)
+    assert int(g2[0, 14]) == eos and (g2[0, 15:] == 0).all()
+
+
+def test_int8_weight_quant():
+    import deepspeedsyclsupport_amd as ds
+    m = tiny("llama").eval()
+    ids = _ids(B=1)
+    with torch.no_grad():
+        ref = m(ids).logits
+    eng = ds.init_inference(m, dtype=torch.float32, replace_with_kernel_inject=True,
+                            quant={"enabled": True, "weight": {"num_bits": 8}})
+    err = (eng(ids).logits - ref).abs().max().item()
+    assert err < 2e-2 * ref.abs().max().item()
+
+
+def test_native_llama_injection():
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd.models.llama import LlamaConfig, LlamaForCausalLM
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(LlamaConfig(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                     num_attention_heads=4, num_key_value_heads=2)).eval()
+    ids = _ids()
+    with torch.no_grad():
+        ref = m(ids)
+    ref = ref.logits if hasattr(ref, "logits") else ref
+    eng = ds.init_inference(m, dtype=torch.float32)
+    assert eng.injected
+    assert (eng(ids).logits - ref).abs().max().item() < 1e-4
+
+
+def test_config_aliases():
+    from deepspeedsyclsupport_amd.inference.config import DeepSpeedInferenceConfig
+    c = DeepSpeedInferenceConfig(kernel_inject=True, dtype="bf16", mp_size=2, max_tokens=77)
+    assert c.replace_with_kernel_inject and c.dtype == torch.bfloat16
+    assert c.tensor_parallel.tp_size == 2 and c.max_out_tokens == 77
+    with pytest.raises(Exception):
+        DeepSpeedInferenceConfig(not_a_key=1)
+
+
+# ---------------------------------------------------------------------------------------------- tensor parallel
+def _tp_run(kind, inject):
+    import deepspeedsyclsupport_amd as ds
+    m = tiny(kind).eval()
+    ids = _ids()
+    with torch.no_grad():
+        ref = m(ids).logits
+    g_ref = m.generate(ids, max_new_tokens=4, do_sample=False, pad_token_id=0) if inject else None
+    eng = ds.init_inference(m, dtype=torch.float32, replace_with_kernel_inject=inject,
+                            tensor_parallel={"tp_size": 2})
+    out = eng(ids)
+    out = out.logits if hasattr(out, "logits") else out[0]
+    err = (out - ref).abs().max().item()
+    assert err < 1e-4, f"{kind} inject={inject} tp2 err {err}"
+    if inject:
+        assert torch.equal(eng.generate(ids, max_new_tokens=4), g_ref)
+
+
+@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt2"])
+def test_tp2_injected(kind):
+    run_distributed(_tp_run, 2, kind, True)
+
+
+@pytest.mark.parametrize("kind", ["llama", "gpt2", "opt"])
+def test_tp2_autotp(kind):
+    run_distributed(_tp_run, 2, kind, False)
+
+
+# ---------------------------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt_neox"])
+def test_injected_bf16_gpu(kind):
+    import deepspeedsyclsupport_amd as ds
+    m = tiny(kind).eval()
+    ids = _ids(B=3, S=20)
+    with torch.no_grad():
+        ref = m(ids).logits.float()
+    eng = ds.init_inference(m, dtype=torch.bfloat16, replace_with_kernel_inject=True)
+    out = eng(ids.cuda()).logits.float().cpu()
+    assert (out - ref).abs().max().item() < 0.05 * ref.abs().max().item() + 0.02
+    # decode through the paged HIP kernel: teacher-force the HF prompt+continuation and compare last-token logits
+    g = eng.generate(ids.cuda(), max_new_tokens=8).cpu()
+    with torch.no_grad():
+        full = m(g[:, :-1]).logits[:, -1].float()
+    step_logits = eng(g[:, :-1].cuda()).logits[:, -1].float().cpu()
+    assert (step_logits - full).abs().max().item() < 0.05 * full.abs().max().item() + 0.02
+
+
+@pytest.mark.gpu
+def test_decode_graph_matches_eager_gpu():
+    import deepspeedsyclsupport_amd as ds
+    m = tiny("llama").eval()
+    ids = _ids(B=4, S=16).cuda()
+    e1 = ds.init_inference(m, dtype=torch.bfloat16, replace_with_kernel_inject=True)
+    e2 = ds.init_inference(m, dtype=torch.bfloat16, replace_with_kernel_inject=True, enable_cuda_graph=True)
+    a = e1.generate(ids, max_new_tokens=12)
+    b = e2.generate(ids, max_new_tokens=12)
+    assert e2.cuda_graph_created
+    assert torch.equal(a, b)

@@ -235,3 +235,111 @@ def test_cross_entropy(V, dtype):
     loss.backward()
     lr_.backward()
     torch.testing.assert_close(logits.grad.float(), lf.grad, **TOL[dtype])
+
+
+# ------------------------------------------------------------------------------------------------ inference kernels
+def _paged_setup(B, Hk, D, BS, lens, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    maxb = max((L + BS - 1) // BS for L in lens)
+    nb = B * maxb + 3
+    kc = torch.randn(nb, Hk, BS, D, device="cuda", generator=g).bfloat16()
+    vc = torch.randn(nb, Hk, BS, D, device="cuda", generator=g).bfloat16()
+    perm = torch.randperm(nb, device="cuda", generator=g)[:B * maxb].to(torch.int32).view(B, maxb)
+    return kc, vc, perm.contiguous(), maxb
+
+
+def _paged_ref(q, kc, vc, bt, lens, scale, alibi=None, window=0):
+    B, Hq, D = q.shape
+    Hk, BS = kc.shape[1], kc.shape[2]
+    out = torch.empty(B, Hq, D, device="cuda")
+    for b in range(B):
+        L = lens[b]
+        nblk = (L + BS - 1) // BS
+        ids = bt[b, :nblk].long()
+        k = kc[ids].float().transpose(0, 1).reshape(Hk, -1, D)[:, :L]
+        v = vc[ids].float().transpose(0, 1).reshape(Hk, -1, D)[:, :L]
+        k, v = k.repeat_interleave(Hq // Hk, 0), v.repeat_interleave(Hq // Hk, 0)
+        s = torch.einsum("hd,htd->ht", q[b].float(), k) * scale
+        if alibi is not None:
+            s = s + alibi[:, None] * (torch.arange(L, device="cuda") - (L - 1)).float()[None]
+        if window:
+            s[:, :max(0, L - window)] = float("-inf")
+        out[b] = torch.einsum("ht,htd->hd", s.softmax(-1), v)
+    return out
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("hq,hk", [(8, 8), (32, 8), (8, 1)])
+@pytest.mark.parametrize("lens", [[1, 7, 64], [300, 2049, 5000]])
+def test_paged_decode(D, hq, hk, lens):
+    B, BS = len(lens), 64
+    kc, vc, bt, maxb = _paged_setup(B, hk, D, BS, lens)
+    q = torch.randn(B, hq, D, device="cuda").bfloat16()
+    sl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    out = ops().paged_decode(q, kc, vc, bt, sl, max(lens), scale, None, 0)
+    ref = _paged_ref(q, kc, vc, bt, lens, scale)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_paged_decode_alibi_window_and_capacity():
+    B, hq, hk, D, BS = 3, 8, 8, 128, 16
+    lens = [5, 40, 100]
+    kc, vc, bt, maxb = _paged_setup(B, hk, D, BS, lens, seed=3)
+    q = torch.randn(B, hq, D, device="cuda").bfloat16()
+    sl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    from deepspeedsyclsupport_amd.inference.model_implementations.transformer import alibi_slopes
+    al = alibi_slopes(hq).cuda()
+    # max_len = full block-table capacity (the HIP-graph decode path): empty splits must not perturb the result
+    out = ops().paged_decode(q, kc, vc, bt, sl, maxb * BS, 0.1, al, 32)
+    ref = _paged_ref(q, kc, vc, bt, lens, 0.1, al, 32)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_kv_append():
+    B, n, hk, D, BS = 3, 5, 4, 128, 16
+    kc, vc, bt, maxb = _paged_setup(B, hk, D, BS, [64, 64, 64])
+    k = torch.randn(B, n, hk, D, device="cuda").bfloat16()
+    v = torch.randn(B, n, hk, D, device="cuda").bfloat16()
+    start = torch.tensor([0, 14, 40], dtype=torch.int32, device="cuda")
+    kr, vr = kc.clone(), vc.clone()
+    ops().kv_append(k, v, kc, vc, bt, start)
+    for b in range(B):
+        for j in range(n):
+            t = int(start[b]) + j
+            blk = int(bt[b, t // BS])
+            kr[blk, :, t % BS] = k[b, j]
+            vr[blk, :, t % BS] = v[b, j]
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+@pytest.mark.parametrize("sym", [True, False])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_quantize_roundtrip(bits, sym, dtype):
+    from deepspeedsyclsupport_amd.ops.quantizer.quantizer import _ref_dequantize, _ref_quantize
+    torch.manual_seed(0)
+    gs = 128
+    x = (torch.randn(64 * gs, device="cuda") * 3).to(dtype)
+    q, s, z = ops().quantize(x, gs, bits, not sym, False, 0)
+    qr, sr, zr = _ref_quantize(x.cpu(), gs, bits, not sym)
+    torch.testing.assert_close(s.cpu(), sr, rtol=1e-5, atol=1e-7)
+    d = ops().dequantize(q, s, z if not sym else None, x.numel(), gs, bits, torch.float32)
+    dr = _ref_dequantize(qr, sr, zr, x.numel(), gs, bits, torch.float32)
+    # kernel and reference may round exact .5 ties differently: allow one quantisation step
+    step = s.repeat_interleave(gs).cpu()
+    assert ((d.cpu() - dr).abs() <= step * 1.01 + 1e-6).all()
+    assert ((x.float() - d).abs() <= s.repeat_interleave(gs) * 0.51 + 1e-5).all()
+
+
+def test_dequant_reduce():
+    from deepspeedsyclsupport_amd.ops.quantizer import quantize
+    torch.manual_seed(0)
+    gs, n, k = 256, 256 * 32, 4
+    xs = [torch.randn(n, device="cuda") for _ in range(k)]
+    qts = [quantize(x, gs, 8) for x in xs]
+    q = torch.cat([t.data for t in qts])
+    s = torch.cat([t.scales for t in qts])
+    out = ops().dequant_reduce(q, s, k, gs, 0.25, torch.float32)
+    ref = sum(x for x in xs) * 0.25
+    torch.testing.assert_close(out, ref, rtol=0, atol=k * 0.25 * float(s.max()) * 0.51)
