@@ -61,6 +61,16 @@ class DSModelSpec:
             self.rotary_dim = self.head_dim
 
 
+SKINNY_MAX_ROWS = 16  # decode batches up to this many token rows use the weight-streaming skinny GEMM kernels
+
+
+def _skinny_rows_ok(m, *ks):
+    """Rows <= 8 run on the VALU GEMV for any K % 8 == 0; 9..16 need the MFMA kernel (every K % 256 == 0)."""
+    if m <= 8:
+        return all(k % 8 == 0 for k in ks)
+    return m <= SKINNY_MAX_ROWS and all(k % 256 == 0 for k in ks)
+
+
 def alibi_slopes(n_heads):
     closest = 2**math.floor(math.log2(n_heads))
     base = 2**(-(2**-(math.log2(closest) - 3)))
@@ -154,32 +164,46 @@ class DSInferenceLayer(nn.Module):
         return x
 
     # ------------------------------------------------------------------------------------------ attention
-    def _attention(self, x, meta: BatchMeta, cache, rope, alibi):
+    def _attend(self, qkv, meta: BatchMeta, cache, rope, alibi):
+        """qkv [B, n, (Hq+2Hk)*D] -> attention output [B, n, Hq*D] (RoPE + cache append + prefill/decode attention)."""
         spec = self.spec
-        B = x.shape[0]
-        n = meta.n_new
-        D = spec.head_dim
-        qkv = F.linear(x, self._w("qkv_w"), self.qkv_b).view(B, n, self.hq + 2 * self.hk, D)
-        q, k, v = qkv.split([self.hq, self.hk, self.hk], dim=2)
-        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-        if spec.pos in ("rope", "rope_gptj"):
-            inter = spec.pos == "rope_gptj"
-            DF.apply_rotary_pos_emb(q, rope[0], rope[1], position_ids=meta.pos_ids.view(B, n), rotary_dim=spec.rotary_dim,
-                                    interleaved=inter)
-            DF.apply_rotary_pos_emb(k, rope[0], rope[1], position_ids=meta.pos_ids.view(B, n), rotary_dim=spec.rotary_dim,
-                                    interleaved=inter)
+        B, n, D = qkv.shape[0], meta.n_new, spec.head_dim
         kc, vc = cache.k[self.layer_idx], cache.v[self.layer_idx]
-        _kv_append(k, v, kc, vc, meta)
+        k = v = None
+        if qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16:
+            # one fused HIP epilogue: split + RoPE(q, k) + scatter k/v into the paged cache
+            from ...ops.native import hip_ops
+            rot = spec.rotary_dim if spec.pos in ("rope", "rope_gptj") else 0
+            want_kv = meta.prefill_from_zero and n > 1
+            outs = hip_ops().qkv_rope_append(qkv.contiguous(), rope[0] if rot else None, rope[1] if rot else None,
+                                             meta.pos_ids, kc, vc, meta.block_tables, meta.start_pos, n, self.hq,
+                                             self.hk, rot, spec.pos == "rope_gptj", want_kv)
+            q = outs[0].view(B, n, self.hq, D)
+            if want_kv:
+                k, v = outs[1].view(B, n, self.hk, D), outs[2].view(B, n, self.hk, D)
+        else:
+            q, k, v = qkv.view(B, n, self.hq + 2 * self.hk, D).split([self.hq, self.hk, self.hk], dim=2)
+            q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+            if spec.pos in ("rope", "rope_gptj"):
+                inter = spec.pos == "rope_gptj"
+                pos = meta.pos_ids.view(B, n)
+                DF.apply_rotary_pos_emb(q, rope[0], rope[1], position_ids=pos, rotary_dim=spec.rotary_dim,
+                                        interleaved=inter)
+                DF.apply_rotary_pos_emb(k, rope[0], rope[1], position_ids=pos, rotary_dim=spec.rotary_dim,
+                                        interleaved=inter)
+            _kv_append(k, v, kc, vc, meta)
         scale = 1.0 / math.sqrt(D)
         if meta.prefill_from_zero and n > 1:
             o = _prefill_attention(q, k, v, scale, alibi, spec.sliding_window)
         elif n == 1:
             o = _decode_attention(q.view(B, self.hq, D), kc, vc, meta, scale, alibi, spec.sliding_window)
-            o = o.view(B, 1, self.hq, D)
         else:
             o = _cached_attention(q, kc, vc, meta, scale, alibi, spec.sliding_window)
-        o = o.reshape(B, n, self.hq * D)
-        out = F.linear(o, self._w("o_w"))
+        return o.reshape(B, n, self.hq * D)
+
+    def _attention(self, x, meta: BatchMeta, cache, rope, alibi):
+        qkv = F.linear(x, self._w("qkv_w"), self.qkv_b)
+        out = F.linear(self._attend(qkv, meta, cache, rope, alibi), self._w("o_w"))
         out = self._allreduce(out)
         if self.o_b is not None:
             out = out + self.o_b
@@ -197,8 +221,47 @@ class DSInferenceLayer(nn.Module):
             out = out + self.fc2_b
         return out
 
+    # ------------------------------------------------------------------------------------------ decode fast path
+    def _skinny_ok(self, h):
+        spec = self.spec
+        return (h.is_cuda and h.dtype == torch.bfloat16 and not self.quant and spec.norm == "rms"
+                and not spec.parallel_residual and _skinny_rows_ok(h.numel() // h.shape[-1], spec.hidden_size,
+                                                                    spec.intermediate_size // self.tp,
+                                                                    self.hq * spec.head_dim))
+
+    def _forward_skinny(self, h, residual, meta, cache, rope, alibi):
+        """Decode (<= 8 token rows): 4 weight-streaming GEMVs with RMSNorm / residual / gated activation fused into
+        their input stage, plus the fused QKV epilogue and the paged decode attention."""
+        from ...ops.native import hip_ops
+        from ...ops.transformer.functional import ACT_CODES
+        ops, eps, tp1 = hip_ops(), self.spec.norm_eps, self.tp == 1
+        res1 = torch.empty_like(h)
+        qkv = ops.skinny_gemm(h, self.qkv_w, self.qkv_b, None, 1, False, 0, residual, self.ln1_w, eps, res1)
+        attn = self._attend(qkv, meta, cache, rope, alibi)
+        o = ops.skinny_gemm(attn, self.o_w, self.o_b if tp1 else None, None, 0, False, 0, None, None, 0.0, None)
+        if not tp1:
+            o = self._allreduce(o)
+            if self.o_b is not None:
+                o = o + self.o_b
+        res2 = torch.empty_like(h)
+        if self.spec.gated_mlp:  # gate/up rows paired in-kernel: writes act(gate) * up directly
+            mid = ops.skinny_gemm(o, self.fc1_w, self.fc1_b, None, 1, True, ACT_CODES[self.spec.act], res1,
+                                  self.ln2_w, eps, res2)
+        else:
+            mid = DF.bias_activation(
+                ops.skinny_gemm(o, self.fc1_w, self.fc1_b, None, 1, False, 0, res1, self.ln2_w, eps, res2), None,
+                self.spec.act)
+        down = ops.skinny_gemm(mid, self.fc2_w, self.fc2_b if tp1 else None, None, 0, False, 0, None, None, 0.0, None)
+        if not tp1:
+            down = self._allreduce(down)
+            if self.fc2_b is not None:
+                down = down + self.fc2_b
+        return down, res2
+
     def forward(self, h, residual, meta, cache, rope, alibi):
         """Pre-norm block. Returns (block_output, residual) where the caller adds them (fused in the next norm)."""
+        if self._skinny_ok(h):
+            return self._forward_skinny(h, residual, meta, cache, rope, alibi)
         if self.spec.parallel_residual:
             x = h if residual is None else h + residual
             a_in = self._norm(x, self.ln1_w, self.ln1_b)
@@ -364,7 +427,9 @@ class DSInferenceModel(nn.Module):
         return h
 
     def _logits(self, h):
-        logits = F.linear(h, self.lm_head, self.lm_head_b)
+        return self._gather_vocab(F.linear(h, self.lm_head, self.lm_head_b))
+
+    def _gather_vocab(self, logits):
         if self.tp_size > 1:
             parts = [torch.empty_like(logits) for _ in range(self.tp_size)]
             dist.all_gather(parts, logits.contiguous(), group=self.tp_group)
@@ -379,14 +444,22 @@ class DSInferenceModel(nn.Module):
         rope = (self.rope_cos, self.rope_sin)
         for layer in self.layers:
             h, residual = layer(h, residual, meta, self.cache, rope, self.alibi)
+        if not all_logits:
+            h = h[:, -1].contiguous()
+            residual = residual[:, -1].contiguous() if residual is not None else None
+            if (h.is_cuda and h.dtype == torch.bfloat16 and self.spec.final_norm and self.spec.norm == "rms"
+                    and _skinny_rows_ok(h.shape[0], self.spec.hidden_size)):
+                # final RMSNorm (+ residual) fused into the LM-head GEMV
+                from ...ops.native import hip_ops
+                logits = hip_ops().skinny_gemm(h, self.lm_head, self.lm_head_b, None, 1, False, 0, residual,
+                                               self.norm_w, self.spec.norm_eps, None)
+                return self._gather_vocab(logits)
         x = h if residual is None else h + residual
         if self.spec.final_norm:
             if self.spec.norm == "rms":
                 x = DF.rms_norm(x, self.norm_w, self.spec.norm_eps)
             else:
                 x = DF.layer_norm(x, self.norm_w, self.norm_b, self.spec.norm_eps)
-        if not all_logits:
-            x = x[:, -1]
         return self._logits(x)
 
     def quantize_weights(self, bits=8, group_size=64):

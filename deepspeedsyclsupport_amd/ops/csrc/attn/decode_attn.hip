@@ -10,7 +10,8 @@
 //    once and serves all G = Hq/Hk query heads of that GQA group from it (no K/V re-read per query head);
 //  * the sequence is split so the launch has >= ~2 workgroups per CU even at batch 1 (256 CUs);
 //  * scores for the slice live in LDS; softmax runs on LDS; P·V streams V rows with 16-B loads, 16 lanes per row;
-//  * partial (max, sum, unnormalised acc) per split are merged by a small combine kernel (log-sum-exp).
+//  * partial (max, sum, unnormalised acc) per split are merged by a small combine kernel (log-sum-exp). (An in-kernel
+//    last-block merge was measured 2x slower: the device-scope fences it needs write back L2.)
 // Optional ALiBi slopes (BLOOM) and a sliding window (Mistral) are applied on the fly.
 #include "../include/ds_hip.h"
 
@@ -79,6 +80,14 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
       }
     }
   }
+  // V rows do not depend on the scores: start the first P.V pass's loads before the softmax phases
+  constexpr int ROWS = THREADS / LPR;
+  const int r = tid / LPR, c = tid % LPR;
+  float vpre[8];
+  if (t0 + r < t1) {
+    const int blk = bt[(t0 + r) / BS], off = (t0 + r) % BS;
+    Vec8<bf16>::load(vc + (((int64_t)blk * Hk + kh) * BS + off) * D + c * 8, vpre);
+  }
   __syncthreads();
   // ---- phase 2: per-head max and sum over the split (one wave per head group, strided)
   const int n = t1 - t0;
@@ -100,17 +109,20 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
   }
   __syncthreads();
   // ---- phase 3: acc[g][d] = sum_t p[g][t] * v[t][d]; LPR lanes per V row, THREADS/LPR rows in flight
-  constexpr int ROWS = THREADS / LPR;
-  const int r = tid / LPR, c = tid % LPR;
   float acc[MAXG][8];
 #pragma unroll
   for (int g = 0; g < MAXG; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   for (int t = t0 + r; t < t1; t += ROWS) {
-    const int blk = bt[t / BS], off = t % BS;
     float vv[8];
-    Vec8<bf16>::load(vc + (((int64_t)blk * Hk + kh) * BS + off) * D + c * 8, vv);
+    if (t == t0 + r) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vv[j] = vpre[j];
+    } else {
+      const int blk = bt[t / BS], off = t % BS;
+      Vec8<bf16>::load(vc + (((int64_t)blk * Hk + kh) * BS + off) * D + c * 8, vv);
+    }
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
       if (g < G) {
@@ -187,6 +199,60 @@ __global__ void __launch_bounds__(256) kv_append_kernel(const bf16* __restrict__
   }
 }
 
+// Fused QKV epilogue for inference: split the fused projection output, apply RoPE (rotate-half or GPT-J interleaved,
+// partial rotary dims allowed) to q and k, write q [T, Hq, D] and scatter k/v straight into the paged cache
+// (optionally also returning contiguous k/v for the prefill attention). Replaces split + 3 copies + 2 RoPE launches
+// + kv_append. One workgroup per token; token t belongs to sequence t / n_new at cache slot start_pos[b] + t % n_new.
+__global__ void __launch_bounds__(256) qkv_rope_append_kernel(
+    const bf16* __restrict__ qkv, const float* __restrict__ cosT, const float* __restrict__ sinT,
+    const int* __restrict__ pos, bf16* __restrict__ q_out, bf16* __restrict__ k_out, bf16* __restrict__ v_out,
+    bf16* __restrict__ kc, bf16* __restrict__ vc, const int* __restrict__ block_table,
+    const int* __restrict__ start_pos, int n_new, int Hq, int Hk, int D, int rot, int interleaved, int BS,
+    int max_blocks) {
+  // grid = (tokens, head groups): 256 threads cover 256 / (D/2) heads of one token, one thread per element pair
+  const int H3 = Hq + 2 * Hk, half = D / 2, rh = rot / 2;
+  const int tph = half < (int)blockDim.x ? half : (int)blockDim.x;
+  const int t = blockIdx.x, h = blockIdx.y * (blockDim.x / tph) + threadIdx.x / tph, b = t / n_new, j = t % n_new;
+  if (h >= H3) return;
+  const bf16* src = qkv + ((int64_t)t * H3 + h) * D;
+  bf16* dst;
+  bf16* extra = nullptr;
+  if (h < Hq) {
+    dst = q_out + ((int64_t)t * Hq + h) * D;
+  } else {
+    const bool isk = h < Hq + Hk;
+    const int kh = isk ? h - Hq : h - Hq - Hk;
+    const int slot = start_pos[b] + j;
+    const int blk = block_table[(int64_t)b * max_blocks + slot / BS], off = slot % BS;
+    dst = (isk ? kc : vc) + (((int64_t)blk * Hk + kh) * BS + off) * D;
+    if (isk ? k_out : v_out) extra = (isk ? k_out : v_out) + ((int64_t)t * Hk + kh) * D;
+  }
+  const int p = pos[t];
+  for (int i = threadIdx.x % tph; i < half; i += tph) {
+    int d0, d1;
+    if (i < rh) {
+      d0 = interleaved ? 2 * i : i;
+      d1 = interleaved ? 2 * i + 1 : i + rh;
+    } else {
+      d0 = rot + 2 * (i - rh);
+      d1 = d0 + 1;
+    }
+    float a = (float)src[d0], c = (float)src[d1];
+    if (i < rh && h < Hq + Hk) {
+      const float cs = cosT[(int64_t)p * rh + i], sn = sinT[(int64_t)p * rh + i];
+      const float a2 = a * cs - c * sn;
+      c = c * cs + a * sn;
+      a = a2;
+    }
+    dst[d0] = (bf16)a;
+    dst[d1] = (bf16)c;
+    if (extra) {
+      extra[d0] = (bf16)a;
+      extra[d1] = (bf16)c;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int ds_paged_decode_splits(int B, int Hk, int max_len) {
@@ -232,6 +298,19 @@ extern "C" int ds_kv_append(const void* k, const void* v, void* kc, void* vc, co
   const int grid = ds_grid_for((int64_t)B * n_new * Hk * (D / 8), 256);
   hipLaunchKernelGGL(kv_append_kernel, dim3(grid), dim3(256), 0, s, (const bf16*)k, (const bf16*)v, (bf16*)kc,
                      (bf16*)vc, block_table, start_pos, B, n_new, Hk, D, BS, max_blocks);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ds_qkv_rope_append(const void* qkv, const float* cosT, const float* sinT, const int* pos, void* q_out,
+                                  void* k_out, void* v_out, void* kc, void* vc, const int* block_table,
+                                  const int* start_pos, int T, int n_new, int Hq, int Hk, int D, int rot,
+                                  int interleaved, int BS, int max_blocks, hipStream_t s) {
+  if (D % 2 || rot % 2 || rot > D || (D - rot) % 2 || T <= 0) return T == 0 ? 0 : (int)hipErrorInvalidValue;
+  const int tph = D / 2 < 256 ? D / 2 : 256, hpb = 256 / tph;
+  hipLaunchKernelGGL(qkv_rope_append_kernel, dim3(T, (Hq + 2 * Hk + hpb - 1) / hpb), dim3(256), 0, s, (const bf16*)qkv, cosT, sinT, pos,
+                     (bf16*)q_out, (bf16*)k_out, (bf16*)v_out, (bf16*)kc, (bf16*)vc, block_table, start_pos, n_new,
+                     Hq, Hk, D, rot, interleaved, BS, max_blocks);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -8,6 +8,15 @@
 
 extern "C" {
 int ds_paged_decode_splits(int, int, int);
+int ds_skinny_gemm(const void*, const void*, const void*, const void*, const void*, const void*, void*, void*, int, int,
+                   int, int, int, int, float, hipStream_t);
+int ds_skinny_fits_lds(int, int);
+int ds_skinny_mfma_ok(int, int, int);
+int ds_skinny_mfma(const void*, const void*, const void*, const void*, const void*, const void*, void*, void*, int, int,
+                   int, int, int, int, float, hipStream_t);
+int ds_rms_fwd(const void*, const void*, const void*, void*, void*, float*, int64_t, int, float, int, hipStream_t);
+int ds_qkv_rope_append(const void*, const float*, const float*, const int*, void*, void*, void*, void*, void*,
+                       const int*, const int*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ds_paged_decode(const void*, const void*, const void*, const int*, const int*, const float*, float*, float*, void*,
                     int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int ds_kv_append(const void*, const void*, void*, void*, const int*, const int*, int, int, int, int, int, int,
@@ -109,7 +118,96 @@ Tensor dequant_reduce(Tensor q, Tensor scales, int64_t nsrc, int64_t gs, double 
 }
 }  // namespace
 
+// DS_SKINNY_VALU=1 (or skinny_force_valu(True)) routes every skinny GEMM to the VALU kernel (A/B testing).
+bool force_valu = getenv("DS_SKINNY_VALU") != nullptr;
+void skinny_force_valu(bool v) { force_valu = v; }
+
+// y [M, N] = X . W^T for M <= 16 rows (decode). in_mode 0: X = x; 1: X = RMSNorm(x (+ r)) * nw (res_out <- x + r).
+// gated: W is a fused [gate; up] weight (N = 2I) and y = act(X.gate^T) * (X.up^T) of width I.
+Tensor skinny_gemm(Tensor x, Tensor w, OptT bias, OptT add, int64_t in_mode, bool gated, int64_t act, OptT r, OptT nw,
+                   double eps, OptT res_out) {
+  need(x, "x"); need(w, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "skinny_gemm: bf16 only");
+  const int N = (int)w.size(0), K = (int)w.size(1);
+  TORCH_CHECK(x.size(-1) == K, "skinny_gemm: inner dim mismatch");
+  const int M = (int)(x.numel() / K);
+  TORCH_CHECK(M >= 1 && M <= 16, "skinny_gemm: M must be in [1, 16]");
+  TORCH_CHECK(!gated || N % 2 == 0, "gated skinny_gemm needs an even N");
+  auto sizes = x.sizes().vec();
+  sizes.back() = gated ? N / 2 : N;
+  auto y = torch::empty(sizes, x.options());
+  auto ptr = [](const OptT& t) -> const void* { return t.has_value() ? t->data_ptr() : nullptr; };
+  for (auto* t : {&bias, &add, &r, &nw, &res_out})
+    if (t->has_value()) need(**t, "skinny_gemm operand");
+  const void* xin = x.data_ptr();
+  const void* rin = ptr(r);
+  Tensor normed;
+  bool mfma = !force_valu && ds_skinny_mfma_ok(M, K, (int)in_mode);
+  if (in_mode == 1 && !mfma && !(M <= 8 && ds_skinny_fits_lds(M, K))) {
+    // activations too large to stage in LDS: normalise with the RMSNorm kernel, then a plain skinny GEMM
+    normed = torch::empty_like(x);
+    auto rstd = torch::empty({M}, x.options().dtype(at::kFloat));
+    // the fused-residual RMSNorm kernel always writes x + r: give it a scratch buffer when the caller wants none
+    Tensor res_scratch;
+    void* rdst = nullptr;
+    if (rin) {
+      if (res_out.has_value()) {
+        rdst = res_out->data_ptr();
+      } else {
+        res_scratch = torch::empty_like(x);
+        rdst = res_scratch.data_ptr();
+      }
+    }
+    check(ds_rms_fwd(x.data_ptr(), rin, nw->data_ptr(), normed.data_ptr(), rdst, rstd.data_ptr<float>(), M, K,
+                     (float)eps, 1, stream()), "rms_fwd");
+    if (res_out.has_value() && !r.has_value()) res_out->copy_(x);
+    xin = normed.data_ptr();
+    rin = nullptr;
+    in_mode = 0;
+    mfma = !force_valu && ds_skinny_mfma_ok(M, K, 0);
+  }
+  TORCH_CHECK(mfma || M <= 8, "skinny_gemm: M > 8 needs K % 256 == 0 (MFMA path)");
+  void* ro = in_mode == 1 && res_out.has_value() ? res_out->data_ptr() : nullptr;
+  auto fn = mfma ? ds_skinny_mfma : ds_skinny_gemm;
+  check(fn(w.data_ptr(), xin, rin, ptr(nw), ptr(bias), ptr(add), y.data_ptr(), ro, M, N, K, (int)in_mode,
+           gated ? 1 : 0, (int)act, (float)eps, stream()),
+        "skinny_gemm");
+  return y;
+}
+
+// qkv [T, (Hq+2Hk)*D] -> q [T, Hq, D] roped; k (roped) / v scattered into the paged cache; optional k/v copies.
+std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, Tensor kc, Tensor vc,
+                                    Tensor block_table, Tensor start_pos, int64_t n_new, int64_t Hq, int64_t Hk,
+                                    int64_t rot, bool interleaved, bool want_kv) {
+  need(qkv, "qkv"); need(pos, "pos"); need(kc, "kc"); need(vc, "vc"); need(block_table, "block_table");
+  need(start_pos, "start_pos");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && kc.scalar_type() == at::kBFloat16, "bf16 qkv / cache");
+  const int D = (int)kc.size(3);
+  const int64_t T = qkv.numel() / ((Hq + 2 * Hk) * D);
+  TORCH_CHECK(T * (Hq + 2 * Hk) * D == qkv.numel() && T % n_new == 0, "qkv shape");
+  TORCH_CHECK(kc.size(1) == Hk, "cache kv heads");
+  TORCH_CHECK(rot == 0 || (cos.has_value() && sin.has_value()), "rope tables required");
+  auto q = torch::empty({T, Hq, D}, qkv.options());
+  Tensor k, v;
+  if (want_kv) {
+    k = torch::empty({T, Hk, D}, qkv.options());
+    v = torch::empty({T, Hk, D}, qkv.options());
+  }
+  check(ds_qkv_rope_append(qkv.data_ptr(), rot ? cos->data_ptr<float>() : nullptr,
+                           rot ? sin->data_ptr<float>() : nullptr, pos.data_ptr<int>(), q.data_ptr(),
+                           want_kv ? k.data_ptr() : nullptr, want_kv ? v.data_ptr() : nullptr, kc.data_ptr(),
+                           vc.data_ptr(), block_table.data_ptr<int>(), start_pos.data_ptr<int>(), (int)T, (int)n_new,
+                           (int)Hq, (int)Hk, D, (int)rot, interleaved ? 1 : 0, (int)kc.size(2),
+                           (int)block_table.size(1), stream()),
+        "qkv_rope_append");
+  if (want_kv) return {q, k, v};
+  return {q};
+}
+
 void register_inference_ops(pybind11::module& m) {
+  m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_force_valu", &skinny_force_valu);
+  m.def("qkv_rope_append", &qkv_rope_append);
   m.def("paged_decode", &paged_decode);
   m.def("kv_append", &kv_append);
   m.def("quantize", &quantize);

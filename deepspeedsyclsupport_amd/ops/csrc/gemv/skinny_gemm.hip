@@ -1,0 +1,274 @@
+// Skinny GEMM for decode: y[M, N] = X[M, K] . W[N, K]^T with M <= 8 token rows (bf16 weights, fp32 accumulate).
+//
+// Decode GEMMs are pure weight streams (Llama-2-7B: 13 GB of weights per token step), so this kernel is built for
+// HBM bandwidth, not MFMA:
+//  * the activation rows X are staged ONCE per workgroup into LDS (bf16, <= 80 KB), with the input-side fusion
+//    applied while staging:
+//      IN 0: X = x
+//      IN 1: X = RMSNorm(x (+ r)) * nw  (block-reduced rstd; workgroup 0 also writes x + r = next residual)
+//  * each wave owns a PAIR of output rows at a time (grid capped at 8 workgroups per CU, then persistent) and streams
+//    their weights with 16-byte non-temporal loads, double-buffered in registers (16 loads in flight per lane) so
+//    the next K-slice is in flight while the current one is multiplied against X from LDS;
+//  * output-side fusion: + bias[n] + add[m, n], or (GATED) the pair is (gate_i, up_i) = rows (i, i + N/2) of a
+//    fused gate_up weight and the kernel writes act(gate_i) * up_i directly -> the gated activation never touches HBM.
+// Rows whose X does not fit LDS (large M*K) fall back to reading X through L1/L2 (XLDS = false, IN 0 only).
+#include "ds_hip.h"
+
+namespace {
+
+constexpr int WAVES = 4;                    // waves per workgroup (small WGs pack 3 per CU at ~130 VGPRs)
+constexpr int U = 4;                        // 16-byte chunks per row per pipeline stage
+constexpr int STEP = 64 * 8 * U;            // K elements per stage
+constexpr int LDS_LIMIT = 80 * 1024;        // bytes of staged X per workgroup (2 workgroups per CU)
+
+__device__ __forceinline__ float act_f(float g, int act) {
+  switch (act) {
+    case 0: return g / (1.f + __expf(-g));                                                     // silu
+    case 1: return 0.5f * g * (1.f + tanhf(0.7978845608f * (g + 0.044715f * g * g * g)));      // gelu tanh
+    case 2: return 0.5f * g * (1.f + erff(g * 0.70710678f));                                   // gelu erf
+    case 3: return fmaxf(g, 0.f);                                                              // relu
+    default: return g;
+  }
+}
+
+__device__ __forceinline__ bf16x8 ld_stream(const bf16* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
+}
+
+template <int MM, bool XLDS>
+struct Tile {
+  float acc[MM][2];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int m = 0; m < MM; ++m) acc[m][0] = acc[m][1] = 0.f;
+  }
+  __device__ __forceinline__ static void load(bf16x8 (&w0)[U], bf16x8 (&w1)[U], const bf16* r0, const bf16* r1,
+                                              int base, int K, int lane) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = base + (u * 64 + lane) * 8;
+      if (c < K) {
+        w0[u] = ld_stream(r0 + c);
+        w1[u] = ld_stream(r1 + c);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w0[u][j] = w1[u][j] = (bf16)0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void fma(const bf16x8 (&w0)[U], const bf16x8 (&w1)[U], const bf16* xs, const bf16* xg,
+                                      int base, int K, int M, int lane) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = base + (u * 64 + lane) * 8;
+      if (c >= K) continue;
+      float a[8], b[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[j] = (float)w0[u][j]; b[j] = (float)w1[u][j]; }
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        if (m >= M) break;  // wave-uniform
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>((XLDS ? xs : xg) + (int64_t)m * K + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xf = (float)xv[j];
+          acc[m][0] = fmaf(xf, a[j], acc[m][0]);
+          acc[m][1] = fmaf(xf, b[j], acc[m][1]);
+        }
+      }
+    }
+  }
+};
+
+template <int MM, int IN, bool GATED, bool XLDS>
+__global__ void __launch_bounds__(WAVES * 64) skinny_kernel(
+    const bf16* __restrict__ W, const bf16* __restrict__ x, const bf16* __restrict__ r, const bf16* __restrict__ nw,
+    const bf16* __restrict__ bias, const bf16* __restrict__ add, bf16* __restrict__ y, bf16* __restrict__ res_out,
+    int M, int N, int K, float eps, int act) {
+  extern __shared__ __attribute__((aligned(16))) bf16 xs[];  // [M][K] staged activations
+  __shared__ float red[WAVES][MM];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // first weight tile of this wave's first pair: issued before staging X so HBM latency overlaps the staging
+  const int pairs = GATED ? N / 2 : (N + 1) / 2;
+  int p = blockIdx.x * WAVES + wid;
+  bf16x8 a0[U], a1[U], b0[U], b1[U];
+  auto rows_of = [&](int pp, const bf16*& r0, const bf16*& r1, int& n0, int& n1) {
+    n0 = GATED ? pp : 2 * pp;
+    n1 = GATED ? pp + N / 2 : min(2 * pp + 1, N - 1);
+    r0 = W + (int64_t)n0 * K;
+    r1 = W + (int64_t)n1 * K;
+  };
+  if (p < pairs) {
+    const bf16 *r0, *r1;
+    int n0, n1;
+    rows_of(p, r0, r1, n0, n1);
+    Tile<MM, XLDS>::load(a0, a1, r0, r1, 0, K, lane);
+  }
+
+  // ---------------------------------------------------------------- stage X (with the input-side fusion)
+  if (XLDS) {
+    if (IN == 1) {
+      float rs[MM];
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        if (m >= M) break;
+        float ss = 0.f;
+        for (int c = tid * 8; c < K; c += WAVES * 512) {
+          float v[8], q[8];
+          Vec8<bf16>::load(x + (int64_t)m * K + c, v);
+          if (r) {
+            Vec8<bf16>::load(r + (int64_t)m * K + c, q);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (float)(bf16)(v[j] + q[j]);  // residual add rounds to bf16 (as HF)
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss = fmaf(v[j], v[j], ss);
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) red[wid][m] = ss;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        if (m >= M) break;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += red[w][m];
+        rs[m] = rsqrtf(t / K + eps);
+      }
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        if (m >= M) break;
+        for (int c = tid * 8; c < K; c += WAVES * 512) {
+          float v[8], q[8], g[8];
+          Vec8<bf16>::load(x + (int64_t)m * K + c, v);
+          if (r) {
+            Vec8<bf16>::load(r + (int64_t)m * K + c, q);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (float)(bf16)(v[j] + q[j]);  // residual add rounds to bf16 (as HF)
+          }
+          if (res_out && blockIdx.x == 0) Vec8<bf16>::store(res_out + (int64_t)m * K + c, v);
+          Vec8<bf16>::load(nw + c, g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (float)(bf16)(v[j] * rs[m]) * g[j];  // HF: norm cast, then * weight
+          Vec8<bf16>::store(xs + (int64_t)m * K + c, v);
+        }
+      }
+    } else {
+      for (int i = tid * 8; i < M * K; i += WAVES * 512)
+        *reinterpret_cast<bf16x8*>(xs + i) = *reinterpret_cast<const bf16x8*>(x + i);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- stream weight-row pairs
+  for (bool first = true; p < pairs; p += gridDim.x * WAVES, first = false) {
+    const bf16 *r0, *r1;
+    int n0, n1;
+    rows_of(p, r0, r1, n0, n1);
+    Tile<MM, XLDS> t;
+    t.zero();
+    if (!first) Tile<MM, XLDS>::load(a0, a1, r0, r1, 0, K, lane);
+    for (int base = 0; base < K; base += 2 * STEP) {
+      const bool more = base + STEP < K;
+      if (more) Tile<MM, XLDS>::load(b0, b1, r0, r1, base + STEP, K, lane);
+      t.fma(a0, a1, xs, x, base, K, M, lane);
+      if (more) {
+        if (base + 2 * STEP < K) Tile<MM, XLDS>::load(a0, a1, r0, r1, base + 2 * STEP, K, lane);
+        t.fma(b0, b1, xs, x, base + STEP, K, M, lane);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      if (m >= M) break;
+      const float s0 = wave_sum(t.acc[m][0]);
+      const float s1 = wave_sum(t.acc[m][1]);
+      if (lane == 0) {
+        float o0 = s0 + (bias ? (float)bias[n0] : 0.f);
+        float o1 = s1 + (bias ? (float)bias[n1] : 0.f);
+        if (GATED) {
+          const float g = (float)(bf16)o0, u = (float)(bf16)o1;  // HF rounds the projections to bf16 first
+          const int Nh = N / 2;
+          y[(int64_t)m * Nh + p] = (bf16)(act_f(g, act) * u + (add ? (float)add[(int64_t)m * Nh + p] : 0.f));
+        } else {
+          if (add) o0 += (float)add[(int64_t)m * N + n0];
+          y[(int64_t)m * N + n0] = (bf16)o0;
+          if (n1 != n0) {
+            if (add) o1 += (float)add[(int64_t)m * N + n1];
+            y[(int64_t)m * N + n1] = (bf16)o1;
+          }
+        }
+      }
+    }
+  }
+}
+
+int g_cus = 0;
+
+template <int MM, int IN, bool GATED, bool XLDS>
+int launch(const bf16* W, const bf16* x, const bf16* r, const bf16* nw, const bf16* bias, const bf16* add, bf16* y,
+           bf16* res_out, int M, int N, int K, float eps, int act, hipStream_t s) {
+  if (!g_cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_cus <= 0)
+      g_cus = 256;
+  }
+  const int pairs = GATED ? N / 2 : (N + 1) / 2;
+  // one wave per row pair while that keeps the grid <= 8 workgroups per CU (dynamic dispatch balances the tail);
+  // beyond that the grid is persistent and waves stride over pairs
+  int grid = (pairs + WAVES - 1) / WAVES;
+  if (grid > 8 * g_cus) grid = 8 * g_cus;
+  const size_t lds = XLDS ? (size_t)M * K * sizeof(bf16) : 0;
+  hipLaunchKernelGGL((skinny_kernel<MM, IN, GATED, XLDS>), dim3(grid), dim3(WAVES * 64), lds, s, W, x, r, nw, bias,
+                     add, y, res_out, M, N, K, eps, act);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int MM>
+int dispatch(int in_mode, bool gated, bool xlds, const bf16* W, const bf16* x, const bf16* r, const bf16* nw,
+             const bf16* bias, const bf16* add, bf16* y, bf16* res_out, int M, int N, int K, float eps, int act,
+             hipStream_t s) {
+#define DS_SK(IN, G, XL) return launch<MM, IN, G, XL>(W, x, r, nw, bias, add, y, res_out, M, N, K, eps, act, s)
+  if (xlds) {
+    if (in_mode == 1) {
+      if (gated) DS_SK(1, true, true);
+      DS_SK(1, false, true);
+    }
+    if (gated) DS_SK(0, true, true);
+    DS_SK(0, false, true);
+  }
+  if (in_mode == 1) return (int)hipErrorInvalidValue;
+  if (gated) DS_SK(0, true, false);
+  DS_SK(0, false, false);
+#undef DS_SK
+}
+
+}  // namespace
+
+// Returns hipErrorInvalidValue for IN 1 when X does not fit LDS (caller normalises separately, then uses IN 0).
+extern "C" int ds_skinny_fits_lds(int M, int K) { return (int64_t)M * K * 2 <= LDS_LIMIT; }
+
+extern "C" int ds_skinny_gemm(const void* W, const void* x, const void* r, const void* nw, const void* bias,
+                              const void* add, void* y, void* res_out, int M, int N, int K, int in_mode, int gated,
+                              int act, float eps, hipStream_t s) {
+  if (M < 1 || M > 8 || K % 8 != 0 || in_mode < 0 || in_mode > 1) return (int)hipErrorInvalidValue;
+  if (in_mode == 1 && !nw) return (int)hipErrorInvalidValue;
+  if (gated && (N % 2)) return (int)hipErrorInvalidValue;
+  const bool xlds = ds_skinny_fits_lds(M, K);
+  auto W_ = (const bf16*)W;
+  auto x_ = (const bf16*)x;
+  auto r_ = (const bf16*)r;
+  auto nw_ = (const bf16*)nw;
+  auto b_ = (const bf16*)bias;
+  auto a_ = (const bf16*)add;
+  auto y_ = (bf16*)y;
+  auto ro_ = (bf16*)res_out;
+  const bool g = gated != 0;
+  if (M == 1) return dispatch<1>(in_mode, g, xlds, W_, x_, r_, nw_, b_, a_, y_, ro_, M, N, K, eps, act, s);
+  if (M == 2) return dispatch<2>(in_mode, g, xlds, W_, x_, r_, nw_, b_, a_, y_, ro_, M, N, K, eps, act, s);
+  if (M <= 4) return dispatch<4>(in_mode, g, xlds, W_, x_, r_, nw_, b_, a_, y_, ro_, M, N, K, eps, act, s);
+  return dispatch<8>(in_mode, g, xlds, W_, x_, r_, nw_, b_, a_, y_, ro_, M, N, K, eps, act, s);
+}

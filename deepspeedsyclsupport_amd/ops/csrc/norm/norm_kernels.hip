@@ -345,6 +345,7 @@ extern "C" int ds_norm_bwd_blocks(int64_t rows) { return ds_grid_for((rows + 3) 
 extern "C" int ds_rms_fwd(const void* x, const void* r, const void* w, void* y, void* res_out, float* rstd,
                           int64_t rows, int H, float eps, int dtype, hipStream_t s) {
   if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (r && !res_out) return (int)hipErrorInvalidValue;  // the fused-residual kernel always writes x + r
   if (rows <= 0) return 0;
   const int grid = norm_grid(rows);
   DISPATCH_T(dtype, DISPATCH_NV(H, {
@@ -382,6 +383,7 @@ extern "C" int ds_rms_bwd(const void* dy, const void* x, const void* w, const fl
 extern "C" int ds_ln_fwd(const void* x, const void* r, const void* g, const void* b, void* y, void* res_out,
                          float* mean, float* rstd, int64_t rows, int H, float eps, int dtype, hipStream_t s) {
   if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (r && !res_out) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
   const int grid = norm_grid(rows);
   DISPATCH_T(dtype, DISPATCH_NV(H, {

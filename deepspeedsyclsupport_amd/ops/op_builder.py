@@ -40,6 +40,8 @@ EXTENSIONS = {
             "xent/xent_kernels.hip",
             "attn/decode_attn.hip",
             "quant/quant_kernels.hip",
+            "gemv/skinny_gemm.hip",
+            "gemv/skinny_mfma.hip",
         ],
         "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp"],
     },

@@ -14,37 +14,38 @@ transformers = pytest.importorskip("transformers")
 V = 256
 
 
-def tiny(kind):
+def tiny(kind, H=64):
+    """Tiny random model; 4 heads so head_dim = H / 4 (GPU tests use H=256 -> D=64, the decode kernel path)."""
     T = transformers
     torch.manual_seed(0)
     if kind == "llama":
-        c = T.LlamaConfig(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+        c = T.LlamaConfig(vocab_size=V, hidden_size=H, intermediate_size=2 * H, num_hidden_layers=2,
                           num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
         return T.LlamaForCausalLM(c)
     if kind == "mistral":
-        c = T.MistralConfig(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+        c = T.MistralConfig(vocab_size=V, hidden_size=H, intermediate_size=2 * H, num_hidden_layers=2,
                             num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128,
                             sliding_window=8)
         return T.MistralForCausalLM(c)
     if kind == "qwen2":
-        c = T.Qwen2Config(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+        c = T.Qwen2Config(vocab_size=V, hidden_size=H, intermediate_size=2 * H, num_hidden_layers=2,
                           num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
         return T.Qwen2ForCausalLM(c)
     if kind == "gpt2":
-        return T.GPT2LMHeadModel(T.GPT2Config(vocab_size=V, n_embd=64, n_layer=2, n_head=4, n_positions=128,
+        return T.GPT2LMHeadModel(T.GPT2Config(vocab_size=V, n_embd=H, n_layer=2, n_head=4, n_positions=128,
                                               bos_token_id=0, eos_token_id=1))
     if kind == "bloom":
-        return T.BloomForCausalLM(T.BloomConfig(vocab_size=V, hidden_size=64, n_layer=2, n_head=4))
+        return T.BloomForCausalLM(T.BloomConfig(vocab_size=V, hidden_size=H, n_layer=2, n_head=4))
     if kind == "opt":
-        return T.OPTForCausalLM(T.OPTConfig(vocab_size=V, hidden_size=64, num_hidden_layers=2, ffn_dim=128,
+        return T.OPTForCausalLM(T.OPTConfig(vocab_size=V, hidden_size=H, num_hidden_layers=2, ffn_dim=2 * H,
                                             num_attention_heads=4, max_position_embeddings=128,
-                                            word_embed_proj_dim=64))
+                                            word_embed_proj_dim=H))
     if kind == "gpt_neox":
-        return T.GPTNeoXForCausalLM(T.GPTNeoXConfig(vocab_size=V, hidden_size=64, num_hidden_layers=2,
-                                                    num_attention_heads=4, intermediate_size=128,
+        return T.GPTNeoXForCausalLM(T.GPTNeoXConfig(vocab_size=V, hidden_size=H, num_hidden_layers=2,
+                                                    num_attention_heads=4, intermediate_size=2 * H,
                                                     max_position_embeddings=128))
     if kind == "gptj":
-        return T.GPTJForCausalLM(T.GPTJConfig(vocab_size=V, n_embd=64, n_layer=2, n_head=4, rotary_dim=8,
+        return T.GPTJForCausalLM(T.GPTJConfig(vocab_size=V, n_embd=H, n_layer=2, n_head=4, rotary_dim=8,
                                               n_positions=128, bos_token_id=0, eos_token_id=1))
     raise ValueError(kind)
 
@@ -166,7 +167,7 @@ def test_tp2_autotp(kind):
 @pytest.mark.parametrize("kind", ["llama", "bloom", "gpt_neox"])
 def test_injected_bf16_gpu(kind):
     import deepspeedsyclsupport_amd as ds
-    m = tiny(kind).eval()
+    m = tiny(kind, H=256).eval()
     ids = _ids(B=3, S=20)
     with torch.no_grad():
         ref = m(ids).logits.float()
@@ -184,7 +185,7 @@ def test_injected_bf16_gpu(kind):
 @pytest.mark.gpu
 def test_decode_graph_matches_eager_gpu():
     import deepspeedsyclsupport_amd as ds
-    m = tiny("llama").eval()
+    m = tiny("llama", H=256).eval()
     ids = _ids(B=4, S=16).cuda()
     e1 = ds.init_inference(m, dtype=torch.bfloat16, replace_with_kernel_inject=True)
     e2 = ds.init_inference(m, dtype=torch.bfloat16, replace_with_kernel_inject=True, enable_cuda_graph=True)

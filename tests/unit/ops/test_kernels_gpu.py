@@ -343,3 +343,101 @@ def test_dequant_reduce():
     out = ops().dequant_reduce(q, s, k, gs, 0.25, torch.float32)
     ref = sum(x for x in xs) * 0.25
     torch.testing.assert_close(out, ref, rtol=0, atol=k * 0.25 * float(s.max()) * 0.51)
+
+
+@pytest.fixture(params=["mfma", "valu"])
+def skinny_path(request):
+    ops().skinny_force_valu(request.param == "valu")
+    yield request.param
+    ops().skinny_force_valu(False)
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 12, 16])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (333, 11008), (7, 64), (100, 256), (50, 768)])
+def test_skinny_gemm_plain(M, N, K, skinny_path):
+    if M > 8 and (K % 256 or skinny_path == "valu"):
+        pytest.skip("rows > 8 need the MFMA kernel (K % 256 == 0)")
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+    b = torch.randn(N, device="cuda").bfloat16()
+    add = torch.randn(M, N, device="cuda").bfloat16()
+    y = ops().skinny_gemm(x, w, b, add, 0, False, 0, None, None, 0.0, None)
+    ref = x.float() @ w.float().t() + b.float() + add.float()
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4, 8, 16])
+@pytest.mark.parametrize("with_res", [False, True])
+@pytest.mark.parametrize("K", [4096, 8192])
+def test_skinny_gemm_rmsnorm(M, with_res, K, skinny_path):
+    if M > 8 and skinny_path == "valu":
+        pytest.skip("rows > 8 need the MFMA kernel")
+    torch.manual_seed(1)
+    N, eps = 1000, 1e-5
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    r = torch.randn(M, K, device="cuda").bfloat16() if with_res else None
+    nw = (1 + 0.1 * torch.randn(K, device="cuda")).bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+    res_out = torch.empty_like(x)
+    y = ops().skinny_gemm(x, w, None, None, 1, False, 0, r, nw, eps, res_out)
+    y2 = ops().skinny_gemm(x, w, None, None, 1, False, 0, r, nw, eps, None)  # LM-head form: no residual output
+    torch.testing.assert_close(y2, y, rtol=0, atol=0)
+    h = (x.float() + (r.float() if with_res else 0)).bfloat16().float()
+    normed, _ = R.rms_norm(h, nw.float(), eps)
+    torch.testing.assert_close(y.float(), normed @ w.float().t(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(res_out.float(), h.bfloat16().float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu", "relu"])
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+def test_skinny_gemm_gated(act, M, skinny_path):
+    if M > 8 and skinny_path == "valu":
+        pytest.skip("rows > 8 need the MFMA kernel")
+    from deepspeedsyclsupport_amd.ops.transformer.functional import ACT_CODES
+    torch.manual_seed(2)
+    I, K = 1376, 4096
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(2 * I, K, device="cuda") * 0.02).bfloat16()
+    b = torch.randn(2 * I, device="cuda").bfloat16()
+    y = ops().skinny_gemm(x, w, b, None, 0, True, ACT_CODES[act], None, None, 0.0, None)
+    gu = (x.float() @ w.float().t() + b.float()).bfloat16().float()
+    ref = R.gated_act(gu, ACT_CODES[act])
+    assert y.shape == (M, I)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("rot,interleaved", [(128, False), (32, False), (64, True), (0, False)])
+def test_qkv_rope_append(rot, interleaved):
+    torch.manual_seed(3)
+    B, n, hq, hk, D, BS = 2, 5, 8, 2, 128, 16
+    kc, vc, bt, maxb = _paged_setup(B, hk, D, BS, [64, 64])
+    qkv = torch.randn(B * n, (hq + 2 * hk) * D, device="cuda").bfloat16()
+    start = torch.tensor([3, 20], dtype=torch.int32, device="cuda")
+    pos = (start[:, None] + torch.arange(n, device="cuda", dtype=torch.int32)[None]).reshape(-1).contiguous()
+    cos, sin = R.rope_tables(256, max(rot, 2), device="cuda")
+    kr, vr = kc.clone(), vc.clone()
+    q, k, v = ops().qkv_rope_append(qkv, cos if rot else None, sin if rot else None, pos, kc, vc, bt, start, n, hq,
+                                    hk, rot, interleaved, True)
+    x = qkv.view(B, n, hq + 2 * hk, D).float()
+    qr, krr, vrr = x[:, :, :hq].clone(), x[:, :, hq:hq + hk].clone(), x[:, :, hq + hk:].clone()
+    p = pos.view(B, n).long()
+    if rot:
+        def rope(t):
+            if interleaved:
+                c, s = cos[p][:, :, None, :], sin[p][:, :, None, :]
+                a, b_ = t[..., 0:rot:2].clone(), t[..., 1:rot:2].clone()
+                t[..., 0:rot:2], t[..., 1:rot:2] = a * c - b_ * s, b_ * c + a * s
+                return t
+            return R.apply_rope_half(t, cos, sin, p)
+        qr, krr = rope(qr), rope(krr)
+    torch.testing.assert_close(q.float().view(B, n, hq, D), qr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(k.float().view(B, n, hk, D), krr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(v.float().view(B, n, hk, D), vrr, rtol=0, atol=0)
+    for b in range(B):
+        for j in range(n):
+            t = int(start[b]) + j
+            blk = int(bt[b, t // BS])
+            kr[blk, :, t % BS] = k.view(B, n, hk, D)[b, j]
+            vr[blk, :, t % BS] = v.view(B, n, hk, D)[b, j]
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)
