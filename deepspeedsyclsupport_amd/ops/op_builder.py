@@ -210,22 +210,28 @@ class OpBuilder:
         return load(self.EXT)
 
 
-def _mk(name, ext):
-    return type(name, (OpBuilder,), {"NAME": name.replace("Builder", "").lower(), "EXT": ext})
+def _mk(cls_name, op_name, ext):
+    return type(cls_name, (OpBuilder, ), {"NAME": op_name, "EXT": ext})
 
 
-FusedAdamBuilder = _mk("FusedAdamBuilder", "ds_hip_ops")
-FusedLambBuilder = _mk("FusedLambBuilder", "ds_hip_ops")
-FusedLionBuilder = _mk("FusedLionBuilder", "ds_hip_ops")
-TransformerBuilder = _mk("TransformerBuilder", "ds_hip_ops")
-CPUAdamBuilder = _mk("CPUAdamBuilder", "ds_cpu_ops")
-CPUAdagradBuilder = _mk("CPUAdagradBuilder", "ds_cpu_ops")
-CPULionBuilder = _mk("CPULionBuilder", "ds_cpu_ops")
-AsyncIOBuilder = _mk("AsyncIOBuilder", "ds_cpu_ops")
-ShareMemCommBuilder = _mk("ShareMemCommBuilder", "ds_cpu_ops")
-
-ALL_OPS = {
-    b.NAME: b
-    for b in (FusedAdamBuilder, FusedLambBuilder, FusedLionBuilder, TransformerBuilder, CPUAdamBuilder,
-              CPUAdagradBuilder, CPULionBuilder, AsyncIOBuilder, ShareMemCommBuilder)
+# reference builder class -> (op NAME, extension that provides it on MI355X)
+_BUILDERS = {
+    "FusedAdamBuilder": ("fused_adam", "ds_hip_ops"),
+    "FusedLambBuilder": ("fused_lamb", "ds_hip_ops"),
+    "FusedLionBuilder": ("fused_lion", "ds_hip_ops"),
+    "TransformerBuilder": ("transformer", "ds_hip_ops"),
+    "StochasticTransformerBuilder": ("stochastic_transformer", "ds_hip_ops"),
+    "InferenceBuilder": ("transformer_inference", "ds_hip_ops"),
+    "InferenceCoreBuilder": ("inference_core_ops", "ds_hip_ops"),
+    "RaggedOpsBuilder": ("ragged_device_ops", "ds_hip_ops"),
+    "QuantizerBuilder": ("quantizer", "ds_hip_ops"),
+    "CPUAdamBuilder": ("cpu_adam", "ds_cpu_ops"),
+    "CPUAdagradBuilder": ("cpu_adagrad", "ds_cpu_ops"),
+    "CPULionBuilder": ("cpu_lion", "ds_cpu_ops"),
+    "AsyncIOBuilder": ("async_io", "ds_cpu_ops"),
+    "ShareMemCommBuilder": ("deepspeed_shm_comm", "ds_cpu_ops"),
 }
+for _cls, (_name, _ext) in _BUILDERS.items():
+    globals()[_cls] = _mk(_cls, _name, _ext)
+
+ALL_OPS = {globals()[c].NAME: globals()[c] for c in _BUILDERS}

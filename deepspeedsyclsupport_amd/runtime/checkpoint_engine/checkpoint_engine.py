@@ -39,9 +39,9 @@ class TorchCheckpointEngine(CheckpointEngine):
         torch.save(state_dict, path)
 
     def load(self, path: str, map_location=None):
-        # our own checkpoints contain python objects (loss scaler, config); weights_only=False is only used on
-        # files this framework wrote (see load_checkpoint docs); user files go through safe loaders
-        return torch.load(path, map_location=map_location, weights_only=False)
+        # checkpoints hold only tensors / containers / primitives (the loss scaler is saved as a dict), so they load
+        # with the non-executing loader
+        return torch.load(path, map_location=map_location, weights_only=True)
 
 
 def _to_host(obj):

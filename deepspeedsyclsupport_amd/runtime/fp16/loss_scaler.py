@@ -28,6 +28,20 @@ class LossScalerBase:
     def backward(self, loss, retain_graph=False):
         (loss * self.loss_scale).backward(retain_graph=retain_graph)
 
+    # plain-dict state so checkpoints stay loadable with torch.load(weights_only=True)
+    def state_dict(self):
+        d = {k: (str(v) if isinstance(v, torch.dtype) else v) for k, v in vars(self).items()}
+        d["type"] = type(self).__name__
+        return d
+
+    def load_state_dict(self, d):
+        for k, v in d.items():
+            if k == "type":
+                continue
+            if k == "dtype" and isinstance(v, str):
+                v = getattr(torch, v.replace("torch.", ""))
+            setattr(self, k, v)
+
 
 class LossScaler(LossScalerBase):
 

@@ -240,9 +240,12 @@ class FlatZeroOptimizer:
                           self.device, self.dtype, d["module"], dp_group=pg)
             self.groups.append(g)
         self.param_group = {}
+        import weakref
+        ref = weakref.ref(self)
         for g in self.groups:
             for i, p in enumerate(g.params):
                 self.param_group[id(p)] = (g, i)
+                p._ds_zero_optimizer = ref  # lets utils.tensor_fragment.safe_get_* find the owner
         self._materialize_buffers()
 
     @torch.no_grad()
@@ -745,14 +748,29 @@ class FlatZeroOptimizer:
     def scale_if_loss(self, loss):
         return loss * self.loss_scaler.loss_scale if self.dtype == torch.float16 else loss
 
+    # ---------------------------------------------------------------- per-parameter views of flat fp32 state
+    _STATE_IDX = {"exp_avg": 0, "exp_avg_sq": 1}
+
+    def _state_src(self, key):
+        """fetch(og, on_host) -> flat fp32 tensor holding `key` ('fp32' master or an optimizer state) for og."""
+        def fetch(og, on_host):
+            if key == "fp32":
+                return (self.master_host if on_host else self.master)[og]
+            if on_host:
+                st = self.host_states.get(og)
+                return None if st is None else st[self._STATE_IDX[key]]
+            st = self.optimizer.state.get(self.fp32_flat[og], {})
+            return st.get(key)
+        return fetch
+
     @torch.no_grad()
-    def get_full_fp32_param(self, p):
-        """Gather the fp32 master value of one parameter (reference `safe_get_full_fp32_param`)."""
+    def _gather_param(self, p, fetch):
         g, i = self.param_group[id(p)]
         seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
         for (s, e, og, moff, on_host) in g.runs:
-            src = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
-            seg32[s:e].copy_(src)
+            src = fetch(og, on_host)
+            if src is not None:
+                seg32[s:e].copy_(src[moff:moff + e - s])
         if g.partition:
             full = torch.empty(g.padded, dtype=torch.float32, device=self.device)
             dist.all_gather_into_tensor(full, seg32, group=g.dp_group)
@@ -761,7 +779,7 @@ class FlatZeroOptimizer:
         return full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).clone()
 
     @torch.no_grad()
-    def set_full_fp32_param(self, p, value):
+    def _scatter_param(self, p, value, fetch, also_shard=False):
         g, i = self.param_group[id(p)]
         flat = value.reshape(-1).to(torch.float32)
         a = g.offsets[i]
@@ -769,9 +787,47 @@ class FlatZeroOptimizer:
             lo, hi = g.seg_lo + s, g.seg_lo + e
             x0, x1 = max(lo, a), min(hi, a + g.numels[i])
             if x0 < x1:
-                dst = (self.master_host if on_host else self.master)[og]
-                dst[moff + x0 - lo:moff + x1 - lo].copy_(flat[x0 - a:x1 - a])
-                g.shard[x0 - g.seg_lo:x1 - g.seg_lo].copy_(flat[x0 - a:x1 - a])
+                dst = fetch(og, on_host)
+                if dst is not None:
+                    dst[moff + x0 - lo:moff + x1 - lo].copy_(flat[x0 - a:x1 - a])
+                if also_shard:
+                    g.shard[x0 - g.seg_lo:x1 - g.seg_lo].copy_(flat[x0 - a:x1 - a])
+
+    def _local_fragment(self, p, fetch):
+        """Elements of `p` owned by this rank's partition (flat fp32), or None."""
+        g, i = self.param_group[id(p)]
+        a, n = g.offsets[i], g.numels[i]
+        parts = []
+        for (s, e, og, moff, on_host) in g.runs:
+            lo, hi = g.seg_lo + s, g.seg_lo + e
+            x0, x1 = max(lo, a), min(hi, a + n)
+            if x0 < x1:
+                src = fetch(og, on_host)
+                if src is not None:
+                    parts.append(src[moff + x0 - lo:moff + x1 - lo])
+        return torch.cat(parts).clone() if parts else None
+
+    def get_full_fp32_param(self, p):
+        """Gather the fp32 master value of one parameter (reference `safe_get_full_fp32_param`)."""
+        return self._gather_param(p, self._state_src("fp32"))
+
+    def get_full_optimizer_state(self, p, key):
+        return self._gather_param(p, self._state_src(key))
+
+    @torch.no_grad()
+    def set_full_optimizer_state(self, p, value, key):
+        self._scatter_param(p, value, self._state_src(key))
+
+    def get_local_fp32_param(self, p):
+        return self._local_fragment(p, self._state_src("fp32"))
+
+    def get_local_optimizer_state(self, p, key):
+        return self._local_fragment(p, self._state_src(key))
+
+    @torch.no_grad()
+    def set_full_fp32_param(self, p, value):
+        g, i = self.param_group[id(p)]
+        self._scatter_param(p, value, self._state_src("fp32"), also_shard=True)
         if g.persistent and g.partition:
             dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
 
@@ -801,7 +857,8 @@ class FlatZeroOptimizer:
         names = {id(p): n for n, p in self.module.named_parameters()}
         out = []
         for g in self.groups:
-            out.append(dict(seg=g.seg, dp=g.dp, persistent=g.persistent,
+            out.append(dict(seg=g.seg, dp=g.dp, persistent=g.persistent, partition=bool(g.partition),
+                            seg_lo=int(g.seg_lo), padded=int(g.padded),
                             params=[(names.get(id(p), f"param_{id(p)}"), list(p.ds_shape), g.offsets[i], g.numels[i])
                                     for i, p in enumerate(g.params)],
                             runs=[(s, e, og, moff, on_host) for (s, e, og, moff, on_host) in g.runs]))
@@ -811,7 +868,7 @@ class FlatZeroOptimizer:
     def state_dict(self):
         sd = OrderedDict()
         sd[CK.ZERO_STAGE] = self.stage
-        sd[CK.LOSS_SCALER] = self.loss_scaler
+        sd[CK.LOSS_SCALER] = self.loss_scaler.state_dict()
         sd["dynamic_loss_scale"] = self.dynamic_loss_scale
         sd["overflow"] = self.overflow
         sd[CK.CLIP_GRAD] = self.clip_grad
@@ -844,7 +901,11 @@ class FlatZeroOptimizer:
             for og, s in sd.get("host_optimizer_states", {}).items():
                 self.host_states[int(og)] = [s[0].clone(), s[1].clone(), s[2]]
         if CK.LOSS_SCALER in sd:
-            self.loss_scaler = sd[CK.LOSS_SCALER]
+            ls = sd[CK.LOSS_SCALER]
+            if isinstance(ls, dict):
+                self.loss_scaler.load_state_dict(ls)
+            else:
+                self.loss_scaler = ls
         self.dynamic_loss_scale = sd.get("dynamic_loss_scale", self.dynamic_loss_scale)
         self.overflow = sd.get("overflow", False)
         if load_from_fp32_weights:

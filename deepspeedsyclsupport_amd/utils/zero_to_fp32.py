@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Consolidate a ZeRO checkpoint into one fp32 state_dict (reference `utils/zero_to_fp32.py:468-592`).
+
+Standalone on purpose (the engine copies it next to every checkpoint): needs only torch.
+
+    python zero_to_fp32.py <checkpoint_dir> <output_file> [-t TAG] [--safe_serialization]
+
+Each rank's `*_optim_states.pt` holds its fp32 master partitions (`single_partition_of_fp32_groups`, one flat
+tensor per optimizer group) plus a layout descriptor (`ds_flat_layout`): for every flat parameter group, the
+per-rank segment size / offset, which slices ("runs") of the segment live in which optimizer-group master at which
+offset (or in the host master for Twin-Flow / offload runs), and (name, shape, offset, numel) of every parameter.
+Reassembly = concatenate the ranks' segments per group, then slice parameters out. Files are read with
+`torch.load(weights_only=True)`.
+"""
+import argparse
+import glob
+import os
+import re
+from collections import OrderedDict
+
+import torch
+
+OPTIM_FILE_SUFFIX = "_optim_states.pt"
+MODEL_FILE_SUFFIX = "_model_states.pt"
+FLAT_LAYOUT = "ds_flat_layout"
+SINGLE_PARTITION_OF_FP32_GROUPS = "single_partition_of_fp32_groups"
+OPTIMIZER_STATE_DICT = "optimizer_state_dict"
+BUFFER_NAMES = "buffer_names"
+
+
+def _load(path):
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def _rank_of(path):
+    m = re.search(r"zero_pp_rank_(\d+)_", os.path.basename(path))
+    return int(m.group(1)) if m else 0
+
+
+def get_optim_files(ckpt_dir):
+    files = sorted(glob.glob(os.path.join(ckpt_dir, f"*{OPTIM_FILE_SUFFIX}")), key=_rank_of)
+    if not files:
+        raise FileNotFoundError(f"no *{OPTIM_FILE_SUFFIX} files in {ckpt_dir}")
+    return files
+
+
+def get_model_state_file(ckpt_dir):
+    files = sorted(glob.glob(os.path.join(ckpt_dir, f"*{MODEL_FILE_SUFFIX}")))
+    if not files:
+        raise FileNotFoundError(f"no *{MODEL_FILE_SUFFIX} files in {ckpt_dir}")
+    return files[0]
+
+
+def _resolve(checkpoint_dir, tag):
+    if tag is None:
+        latest = os.path.join(checkpoint_dir, "latest")
+        if not os.path.isfile(latest):
+            raise ValueError(f"no 'latest' file in {checkpoint_dir}; pass tag explicitly")
+        with open(latest) as f:
+            tag = f.read().strip()
+    path = os.path.join(checkpoint_dir, tag)
+    if not os.path.isdir(path):
+        raise FileNotFoundError(f"directory {path} does not exist")
+    return path
+
+
+def _get_fp32_state_dict_from_zero_checkpoint(ds_checkpoint_dir, exclude_frozen_parameters=False):
+    files = get_optim_files(ds_checkpoint_dir)
+    states = [_load(f)[OPTIMIZER_STATE_DICT] for f in files]
+    layout0 = states[0][FLAT_LAYOUT]
+    out = OrderedDict()
+    for gi, g in enumerate(layout0):
+        full = torch.zeros(g["padded"], dtype=torch.float32)
+        if g["partition"]:
+            owners = range(len(states))
+        else:
+            owners = [0]  # replicated group: every rank holds the whole segment
+        for r in owners:
+            st = states[r]
+            lg = st[FLAT_LAYOUT][gi]
+            masters = st[SINGLE_PARTITION_OF_FP32_GROUPS]
+            host = st.get("fp32_host_partitions") or []
+            for (s, e, og, moff, on_host) in lg["runs"]:
+                src = host[og] if on_host else masters[og]
+                full[lg["seg_lo"] + s:lg["seg_lo"] + e] = src[moff:moff + e - s].float()
+        for name, shape, off, numel in g["params"]:
+            out[name] = full[off:off + numel].view(shape).clone()
+    # buffers (and any non-partitioned tensors) come from the 16-bit model file
+    try:
+        model_sd = _load(get_model_state_file(ds_checkpoint_dir))
+        buffers = set(model_sd.get(BUFFER_NAMES, []) or [])
+        for k, v in (model_sd.get("module") or {}).items():
+            if k in buffers or (k not in out and not exclude_frozen_parameters):
+                out[k] = v.float() if torch.is_floating_point(v) else v
+    except FileNotFoundError:
+        pass
+    return out
+
+
+def get_fp32_state_dict_from_zero_checkpoint(checkpoint_dir, tag=None, exclude_frozen_parameters=False):
+    return _get_fp32_state_dict_from_zero_checkpoint(_resolve(checkpoint_dir, tag), exclude_frozen_parameters)
+
+
+def convert_zero_checkpoint_to_fp32_state_dict(checkpoint_dir, output_file, tag=None,
+                                               exclude_frozen_parameters=False, safe_serialization=False):
+    sd = get_fp32_state_dict_from_zero_checkpoint(checkpoint_dir, tag, exclude_frozen_parameters)
+    if safe_serialization:
+        from safetensors.torch import save_file
+        save_file({k: v.contiguous() for k, v in sd.items()}, output_file)
+    else:
+        torch.save(sd, output_file)
+    return sd
+
+
+def load_state_dict_from_zero_checkpoint(model, checkpoint_dir, tag=None):
+    sd = get_fp32_state_dict_from_zero_checkpoint(checkpoint_dir, tag)
+    model = model.cpu()
+    model.load_state_dict(sd, strict=False)
+    return model
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("checkpoint_dir")
+    ap.add_argument("output_file")
+    ap.add_argument("-t", "--tag", default=None)
+    ap.add_argument("--exclude_frozen_parameters", action="store_true")
+    ap.add_argument("--safe_serialization", action="store_true")
+    a = ap.parse_args()
+    convert_zero_checkpoint_to_fp32_state_dict(a.checkpoint_dir, a.output_file, a.tag, a.exclude_frozen_parameters,
+                                               a.safe_serialization)
