@@ -1,8 +1,12 @@
 """deepspeedsyclsupport_amd — an MI355X-native (gfx950 / ROCm / RCCL-over-xGMI) ZeRO training & inference framework
 with the capabilities and user API of DeepSpeed (`deepspeed.initialize`, `engine.backward/step`, `zero.Init`,
 `init_inference`, ...). See SURVEY.md for the component map and README.md for the design."""
-__version__ = "0.1.0"
-__version_major__, __version_minor__, __version_patch__ = 0, 1, 0
+# API level of the reference release this framework tracks (scripts and elasticity checks compare against it);
+# the MI355X implementation has its own release counter.
+__version__ = "0.12.7"
+__mi355x_version__ = "0.1.0"
+version = __version__
+__version_major__, __version_minor__, __version_patch__ = 0, 12, 7
 __git_hash__ = None
 __git_branch__ = None
 

@@ -211,9 +211,34 @@ class DeepSpeedConfig:
             sp = self._param_dict.get("sequence_parallel", {}).get("size", 1)
             self.world_size = max(dist.get_world_size() // sp, 1)
         self.global_rank = dist.get_rank()
+        self.elasticity_enabled = self._apply_elasticity(self._param_dict)
         self._initialize_params(self._param_dict)
         self._configure_train_batch_size()
         self._do_sanity_check()
+
+    def _apply_elasticity(self, p):
+        """Elastic batch sizing overrides the batch triple (reference `runtime/config.py:723-785`)."""
+        from ..elasticity import compute_elastic_config, elasticity_enabled, ensure_immutable_elastic_config
+        from ..elasticity.config import ElasticityConfigError
+        if not elasticity_enabled(p):
+            return False
+        from .. import __version__
+        ensure_immutable_elastic_config(p["elasticity"])
+        mp = p["elasticity"].get("model_parallel_size", 1)
+        bs, valid, mb = compute_elastic_config(p, __version__, world_size=self.world_size * 1, return_microbatch=True)
+        if mp > 1:
+            pass  # world_size above is already data-parallel
+        ignore = p["elasticity"].get("ignore_non_elastic_batch_info", False)
+        if not ignore:
+            for key in ("train_batch_size", "train_micro_batch_size_per_gpu", "gradient_accumulation_steps"):
+                if key in p:
+                    raise ElasticityConfigError(f"'{key}' must not be set when elasticity is enabled (found "
+                                                f"{p[key]}); set 'ignore_non_elastic_batch_info': true to override")
+        p["train_batch_size"] = bs
+        p["train_micro_batch_size_per_gpu"] = mb
+        p["gradient_accumulation_steps"] = bs // (mb * self.world_size)
+        self.elastic_valid_gpus = valid
+        return True
 
     # --------------------------------------------------------------------------------------- parse
     def _initialize_params(self, p):
