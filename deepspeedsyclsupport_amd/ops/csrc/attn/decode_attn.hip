@@ -50,32 +50,45 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
   constexpr int RPW = 64 / LPR;             // rows per wave instruction
   const int sub = lane / LPR, li = lane % LPR;
   float qv[MAXG][8];
+  // unconditional loads (clamped head index): a guarded load would make the compiler wait on each one in turn
 #pragma unroll
   for (int g = 0; g < MAXG; ++g) {
-    if (g < G) {
-      Vec8<bf16>::load(q + ((int64_t)b * Hq + kh * G + g) * D + li * 8, qv[g]);
+    const int gc = g < G ? g : G - 1;
+    Vec8<bf16>::load(q + ((int64_t)b * Hq + kh * G + gc) * D + li * 8, qv[g]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qv[g][j] *= scale;
-    }
+    for (int j = 0; j < 8; ++j) qv[g][j] *= scale;
   }
-  // ---- phase 1: scores for keys of this split
+  // ---- phase 1: scores for keys of this split (UNR key rows per lane-group in flight per iteration)
+  constexpr int UNR = 4;
   const int* bt = block_table + (int64_t)b * max_blocks;
-  for (int t = t0 + wid * RPW + sub; t < t1; t += (THREADS / 64) * RPW) {
-    const int blk = bt[t / BS], off = t % BS;
-    float kv[8];
-    Vec8<bf16>::load(kc + (((int64_t)blk * Hk + kh) * BS + off) * D + li * 8, kv);
+  const int kstride = (THREADS / 64) * RPW;
+  for (int tb = t0 + wid * RPW + sub; tb < t1; tb += kstride * UNR) {
+    float kv[UNR][8];
+    int blk[UNR];
 #pragma unroll
-    for (int g = 0; g < MAXG; ++g) {
-      if (g < G) {
-        float s = 0.f;
+    for (int u = 0; u < UNR; ++u) blk[u] = bt[min(tb + u * kstride, t1 - 1) / BS];  // clamped: always valid
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s = fmaf(qv[g][j], kv[j], s);
+    for (int u = 0; u < UNR; ++u) {
+      const int tc = min(tb + u * kstride, t1 - 1);
+      Vec8<bf16>::load(kc + (((int64_t)blk[u] * Hk + kh) * BS + tc % BS) * D + li * 8, kv[u]);
+    }
 #pragma unroll
-        for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (li == 0) {
-          if (alibi) s += alibi[kh * G + g] * (float)(t - (T - 1));
-          if (t < tlo) s = -INFINITY;
-          scores[g * MAX_CHUNK + (t - t0)] = s;
+    for (int u = 0; u < UNR; ++u) {
+      const int t = tb + u * kstride;
+      if (t >= t1) continue;  // uniform across the LPR lanes of one key row (the shuffle partners)
+#pragma unroll
+      for (int g = 0; g < MAXG; ++g) {
+        if (g < G) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s = fmaf(qv[g][j], kv[u][j], s);
+#pragma unroll
+          for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+          if (li == 0) {
+            if (alibi) s += alibi[kh * G + g] * (float)(t - (T - 1));
+            if (t < tlo) s = -INFINITY;
+            scores[g * MAX_CHUNK + (t - t0)] = s;
+          }
         }
       }
     }
@@ -114,21 +127,32 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
   for (int g = 0; g < MAXG; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  for (int t = t0 + r; t < t1; t += ROWS) {
-    float vv[8];
-    if (t == t0 + r) {
+  for (int tb = t0 + r; tb < t1; tb += ROWS * UNR) {
+    float vv[UNR][8];
+    int vblk[UNR];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vv[j] = vpre[j];
-    } else {
-      const int blk = bt[t / BS], off = t % BS;
-      Vec8<bf16>::load(vc + (((int64_t)blk * Hk + kh) * BS + off) * D + c * 8, vv);
+    for (int u = 0; u < UNR; ++u) vblk[u] = bt[min(tb + u * ROWS, t1 - 1) / BS];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int tc = min(tb + u * ROWS, t1 - 1);
+      if (u == 0 && tb == t0 + r) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vv[u][j] = vpre[j];
+      } else {
+        Vec8<bf16>::load(vc + (((int64_t)vblk[u] * Hk + kh) * BS + tc % BS) * D + c * 8, vv[u]);
+      }
     }
 #pragma unroll
-    for (int g = 0; g < MAXG; ++g) {
-      if (g < G) {
-        const float p = scores[g * MAX_CHUNK + (t - t0)];
+    for (int u = 0; u < UNR; ++u) {
+      const int t = tb + u * ROWS;
+      if (t >= t1) continue;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(p, vv[j], acc[g][j]);
+      for (int g = 0; g < MAXG; ++g) {
+        if (g < G) {
+          const float p = scores[g * MAX_CHUNK + (t - t0)];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(p, vv[u][j], acc[g][j]);
+        }
       }
     }
   }

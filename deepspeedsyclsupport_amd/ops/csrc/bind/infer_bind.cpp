@@ -118,9 +118,20 @@ Tensor dequant_reduce(Tensor q, Tensor scales, int64_t nsrc, int64_t gs, double 
 }
 }  // namespace
 
-// DS_SKINNY_VALU=1 (or skinny_force_valu(True)) routes every skinny GEMM to the VALU kernel (A/B testing).
-bool force_valu = getenv("DS_SKINNY_VALU") != nullptr;
-void skinny_force_valu(bool v) { force_valu = v; }
+// Skinny-GEMM path policy: 0 = auto, 1 = VALU kernel only, 2 = MFMA kernel only (A/B testing; DS_SKINNY_PATH).
+int skinny_path = getenv("DS_SKINNY_PATH") ? atoi(getenv("DS_SKINNY_PATH")) : 0;
+void skinny_set_path(int64_t p) { skinny_path = (int)p; }
+void skinny_force_valu(bool v) { skinny_path = v ? 1 : 0; }
+
+// auto policy (measured on MI355X, tools/bench_skinny.py): M <= 2 -> VALU kernel (its fused RMSNorm staging and
+// gated epilogue are cheapest there); M > 2 -> RMSNorm once, then the MFMA kernel (per-workgroup normalisation
+// cost grows with M, and VALU FMA throughput runs out)
+static bool use_mfma(int M, int K, int in_mode) {
+  if (skinny_path == 1) return false;
+  if (skinny_path == 2) return ds_skinny_mfma_ok(M, K, in_mode);
+  if (M <= 2 && K % 8 == 0 && (in_mode == 0 || ds_skinny_fits_lds(M, K))) return false;
+  return in_mode == 0 && ds_skinny_mfma_ok(M, K, 0);
+}
 
 // y [M, N] = X . W^T for M <= 16 rows (decode). in_mode 0: X = x; 1: X = RMSNorm(x (+ r)) * nw (res_out <- x + r).
 // gated: W is a fused [gate; up] weight (N = 2I) and y = act(X.gate^T) * (X.up^T) of width I.
@@ -142,8 +153,9 @@ Tensor skinny_gemm(Tensor x, Tensor w, OptT bias, OptT add, int64_t in_mode, boo
   const void* xin = x.data_ptr();
   const void* rin = ptr(r);
   Tensor normed;
-  bool mfma = !force_valu && ds_skinny_mfma_ok(M, K, (int)in_mode);
-  if (in_mode == 1 && !mfma && !(M <= 8 && ds_skinny_fits_lds(M, K))) {
+  bool mfma = use_mfma(M, K, (int)in_mode);
+  const bool valu_fused = skinny_path != 2 && M <= 8 && ds_skinny_fits_lds(M, K) && (skinny_path == 1 || M <= 2);
+  if (in_mode == 1 && !mfma && !valu_fused) {
     // activations too large to stage in LDS: normalise with the RMSNorm kernel, then a plain skinny GEMM
     normed = torch::empty_like(x);
     auto rstd = torch::empty({M}, x.options().dtype(at::kFloat));
@@ -164,7 +176,7 @@ Tensor skinny_gemm(Tensor x, Tensor w, OptT bias, OptT add, int64_t in_mode, boo
     xin = normed.data_ptr();
     rin = nullptr;
     in_mode = 0;
-    mfma = !force_valu && ds_skinny_mfma_ok(M, K, 0);
+    mfma = use_mfma(M, K, 0);
   }
   TORCH_CHECK(mfma || M <= 8, "skinny_gemm: M > 8 needs K % 256 == 0 (MFMA path)");
   void* ro = in_mode == 1 && res_out.has_value() ? res_out->data_ptr() : nullptr;
@@ -207,6 +219,7 @@ std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, 
 void register_inference_ops(pybind11::module& m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_force_valu", &skinny_force_valu);
+  m.def("skinny_set_path", &skinny_set_path);
   m.def("qkv_rope_append", &qkv_rope_append);
   m.def("paged_decode", &paged_decode);
   m.def("kv_append", &kv_append);

@@ -176,7 +176,7 @@ int launch(const bf16* W, const bf16* x, const bf16* r, const bf16* nw, const bf
   static bool attr_set = false;
   if (lds > 64 * 1024 && !attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_mfma_kernel<T, IN, G>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024);
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL((skinny_mfma_kernel<T, IN, G>), dim3(grid), dim3(NW * 64), lds, s, W, x, r, nw, bias, add, y,
@@ -190,7 +190,7 @@ int launch(const bf16* W, const bf16* x, const bf16* r, const bf16* nw, const bf
 // LDS the IN 1 staging needs (bytes); the caller falls back to a separate RMSNorm above the budget.
 extern "C" int ds_skinny_mfma_ok(int M, int K, int in_mode) {
   if (M < 1 || M > 16 || K % (NW * 32) != 0) return 0;
-  if (in_mode == 1 && (int64_t)M * (K + 8) * 2 > 128 * 1024) return 0;
+  if (in_mode == 1 && (int64_t)M * (K + 8) * 2 > 140 * 1024) return 0;  // + 16 KB split-K tiles <= 160 KB
   return 1;
 }
 

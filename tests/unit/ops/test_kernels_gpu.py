@@ -345,11 +345,11 @@ def test_dequant_reduce():
     torch.testing.assert_close(out, ref, rtol=0, atol=k * 0.25 * float(s.max()) * 0.51)
 
 
-@pytest.fixture(params=["mfma", "valu"])
+@pytest.fixture(params=["mfma", "valu", "auto"])
 def skinny_path(request):
-    ops().skinny_force_valu(request.param == "valu")
+    ops().skinny_set_path({"auto": 0, "valu": 1, "mfma": 2}[request.param])
     yield request.param
-    ops().skinny_force_valu(False)
+    ops().skinny_set_path(0)
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 12, 16])
