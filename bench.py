@@ -33,6 +33,8 @@ def parse():
     ap.add_argument("--stage", type=int, default=3)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing (not needed with 288 GB HBM)")
     ap.add_argument("--local_rank", type=int, default=0)
+    ap.add_argument("--host-dryrun", action="store_true",
+                    help="CPU/gloo rehearsal of the multi-rank control flow (tiny model; not a measurement)")
     return ap.parse_args()
 
 
@@ -47,11 +49,25 @@ def main():
     from deepspeedsyclsupport_amd import comm as dist
     from deepspeedsyclsupport_amd.models.llama import LlamaConfig, LlamaForCausalLM, llama2_7b_config, llama2_13b_config
 
-    ds.init_distributed(dist_backend="nccl")
+    ds.init_distributed(dist_backend="gloo" if args.host_dryrun else "nccl")
     rank, world = dist.get_rank(), dist.get_world_size()
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.host_dryrun:
+        dev = torch.device("cpu")
+        args.model, args.seq_len, args.micro_batch = "tiny", min(args.seq_len, 128), min(args.micro_batch, 2)
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    on_gpu = dev.type == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    def mem_gib(peak=False):
+        if not on_gpu:
+            return 0.0
+        return (torch.cuda.max_memory_allocated() if peak else torch.cuda.memory_allocated()) / 2**30
 
     if args.model == "llama2-7b":
         cfg = llama2_7b_config(max_position_embeddings=args.seq_len)
@@ -64,7 +80,7 @@ def main():
     torch.manual_seed(1234)
     # build directly on the GPU in bf16 (fast init; fp32 masters are created by the ZeRO optimizer)
     prev = torch.get_default_dtype()
-    torch.set_default_dtype(torch.bfloat16)
+    torch.set_default_dtype(torch.bfloat16 if on_gpu else torch.float32)
     with torch.device(dev):
         model = LlamaForCausalLM(cfg)
     torch.set_default_dtype(prev)
@@ -92,7 +108,7 @@ def main():
         },
     }
     engine, _, _, _ = ds.initialize(model=model, config=config)
-    log(f"[bench] engine ready in {time.time() - t0:.1f}s; mem {torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+    log(f"[bench] engine ready in {time.time() - t0:.1f}s; mem {mem_gib():.1f} GiB")
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     batches = [torch.randint(0, cfg.vocab_size, (args.micro_batch, args.seq_len), device=dev, generator=g)
@@ -109,18 +125,17 @@ def main():
     for i in range(args.warmup):
         tw = time.time()
         loss = train_step(i)
-        torch.cuda.synchronize()
-        log(f"[bench] warmup {i}: loss={float(loss):.4f} {time.time() - tw:.2f}s "
-            f"peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+        sync()
+        log(f"[bench] warmup {i}: loss={float(loss):.4f} {time.time() - tw:.2f}s peak {mem_gib(True):.1f} GiB")
 
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
     for i in range(args.steps):
         loss = train_step(i)
         if rank == 0 and (i + 1) % max(1, args.steps // 5) == 0:
             log(f"[bench] step {i + 1}/{args.steps}")
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     elapsed = time.perf_counter() - t_start
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -132,7 +147,7 @@ def main():
     tok_s = tokens_per_step * args.steps / elapsed
     flops_tok = cfg.flops_per_token(args.seq_len)
     tflops_gpu = tok_s * flops_tok / world / 1e12
-    peak_mem = torch.cuda.max_memory_allocated() / 2**30
+    peak_mem = mem_gib(True)
     if rank == 0:
         out = {
             "metric": "tokens/sec Llama-2-7B ZeRO-3 at 1/2/4/8 MI355X; peak trainable params/GPU",
