@@ -34,6 +34,16 @@ class ParamCoordinator:
         self.acc = opt.acc
         self._hooks = []
         self.live_numel = 0
+        # ZeRO++ (qwZ quantized weight gather, hpZ intra-node secondary partitions)
+        zc = opt.zc
+        self.qwz = bool(zc is not None and zc.zero_quantized_weights)
+        self.hpz = None
+        if zc is not None and zc.zero_hpz_partition_size > 1 and opt.dp > zc.zero_hpz_partition_size:
+            from ...parallel import groups
+            from .zeropp import HpzState
+            if not groups._zero_param_parallel_is_initialized():
+                groups._create_zero_param_parallel_group(zc.zero_hpz_partition_size)
+            self.hpz = HpzState(groups._get_zero_param_intra_parallel_group())
         install_zero3_linear(opt.module)
         for g in opt.groups:
             if g.persistent or g.module is None:
@@ -57,6 +67,20 @@ class ParamCoordinator:
         self.fetch(m._ds_fetch_group)
 
     # ----------------------------------------------------------------------------------- core
+    def _gather(self, g):
+        """Fill g.full: hpZ intra-node re-gather in backward, qwZ int8 gather, or the plain bf16 all-gather."""
+        hpz = self.hpz if (self.hpz is not None and g.dp_group is self.opt.dp_group) else None
+        if self.in_backward and hpz is not None and hpz.can_use(g):
+            hpz.gather_from_secondary(g)
+            return
+        if self.qwz:
+            from .zeropp import quantized_all_gather
+            quantized_all_gather(g.full, g.shard, g.dp_group)
+        else:
+            dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
+        if hpz is not None and not self.in_backward:
+            hpz.keep_secondary(g)
+
     def _issue(self, g):
         opt = self.opt
         if g.status != ZeroParamStatus.NOT_AVAILABLE:
@@ -66,12 +90,12 @@ class ParamCoordinator:
             self.ag_stream.wait_stream(compute)
             with self.acc.stream(self.ag_stream):
                 g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
-                dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
+                self._gather(g)
                 g.ag_event = self.acc.Event()
                 g.ag_event.record(self.ag_stream)
         else:
             g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
-            dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
+            self._gather(g)
             g.ag_event = None
         g.status = ZeroParamStatus.INFLIGHT
         self.live_numel += g.padded
@@ -103,6 +127,8 @@ class ParamCoordinator:
 
     def release_after_backward(self, g):
         self.release(g)
+        if self.hpz is not None:
+            self.hpz.drop(g)
 
     # ----------------------------------------------------------------------------------- trace / prefetch
     def _trace(self, g):

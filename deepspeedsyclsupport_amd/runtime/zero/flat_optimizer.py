@@ -445,7 +445,11 @@ class FlatZeroOptimizer:
                 comm.mul_(1.0 / self._div())
             if g.partition:
                 out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
-                dist.reduce_scatter_tensor(out, comm, group=g.dp_group)
+                if self.zc is not None and self.zc.zero_quantized_gradients:
+                    from .zeropp import quantized_reduce_scatter  # qgZ: int8 all-to-all + fused dequant-reduce
+                    quantized_reduce_scatter(out, comm, g.dp_group)
+                else:
+                    dist.reduce_scatter_tensor(out, comm, group=g.dp_group)
             else:
                 dist.all_reduce(comm, group=g.dp_group)
                 out = comm[g.seg_lo:g.seg_lo + g.seg]
