@@ -538,8 +538,7 @@ class DeepSpeedEngine(nn.Module):
             if os.path.exists(zpath):
                 zsd = self.checkpoint_engine.load(zpath, map_location="cpu")
                 osd = zsd["optimizer_state_dict"]
-                same_topology = osd.get(CK.PARTITION_COUNT, 1) == (self.optimizer.dp if self.optimizer.partition
-                                                                   else 1)
+                same_topology = osd.get(CK.PARTITION_COUNT, 1) == self.optimizer.partition_count()
                 if same_topology:
                     self.optimizer.load_state_dict(osd, load_optimizer_states=load_optimizer_states)
                 else:

@@ -133,6 +133,7 @@ class FlatZeroOptimizer:
             else torch.device("cpu")
         self.partition = self.stage >= 1 and self.dp > 1
         self.world = dist.get_world_size()
+        self._setup_mics()
         self.comm_dtype = communication_data_type or dtype
         self.gas = gradient_accumulation_steps
         self.is_gradient_accumulation_boundary = True
@@ -193,7 +194,7 @@ class FlatZeroOptimizer:
                 from ...parallel import groups as pgroups
                 self.og_dp_group.append(pgroups._get_expert_data_parallel_group(g["name"]))
             else:
-                self.og_dp_group.append(self.dp_group)
+                self.og_dp_group.append(self.mics_shard_group or self.dp_group)
         groups = []
         if self.stage == 3:
             # one group per module that directly owns trainable params (fetch granularity = module), plus ONE
@@ -450,6 +451,8 @@ class FlatZeroOptimizer:
                     quantized_reduce_scatter(out, comm, g.dp_group)
                 else:
                     dist.reduce_scatter_tensor(out, comm, group=g.dp_group)
+                if self.mics_replica_group is not None and g.dp_group is self.mics_shard_group:
+                    dist.all_reduce(out, group=self.mics_replica_group)
             else:
                 dist.all_reduce(comm, group=g.dp_group)
                 out = comm[g.seg_lo:g.seg_lo + g.seg]
@@ -531,7 +534,41 @@ class FlatZeroOptimizer:
         """Ranks holding an identical copy of each element of this og's local master (1 when partitioned)."""
         pg = self.og_dp_group[og]
         n = dist.get_world_size(pg)
-        return 1 if (self.stage >= 1 and n > 1) else n
+        base = 1 if (self.stage >= 1 and n > 1) else n
+        if self.mics_shard_group is not None and pg is self.mics_shard_group:
+            base *= self.mics_replicas
+        return base
+
+    def partition_count(self):
+        if not self.partition:
+            return 1
+        return self.dp // self.mics_replicas
+
+    # ================================================================================ MiCS
+    def _setup_mics(self):
+        """MiCS (reference `runtime/zero/mics.py`): partition dense params inside groups of `mics_shard_size`
+        consecutive ranks (one xGMI node) and replicate across groups; gradients reduce-scatter inside the shard
+        group, then all-reduce across replicas (the only inter-group traffic)."""
+        self.mics_shard_group = None
+        self.mics_replica_group = None
+        self.mics_replicas = 1
+        S = int(getattr(self.zc, "mics_shard_size", -1) or -1) if self.zc is not None else -1
+        if S <= 1 or S >= self.dp or self.stage < 1:
+            return
+        assert self.dp % S == 0, f"mics_shard_size {S} must divide the data-parallel size {self.dp}"
+        ranks = dist.get_all_ranks_from_group(self.dp_group) if self.dp != self.world else list(range(self.world))
+        me = dist.get_rank()
+        for i in range(self.dp // S):
+            grp = ranks[i * S:(i + 1) * S]
+            g = dist.new_group(grp)
+            if me in grp:
+                self.mics_shard_group = g
+        for j in range(S):
+            grp = ranks[j::S]
+            g = dist.new_group(grp)
+            if me in grp:
+                self.mics_replica_group = g
+        self.mics_replicas = self.dp // S
 
     def _grad_items(self):
         """[(og, moff, n, grad_1d, lp_1d, scale, on_host)] covering every local master element that has a gradient."""
@@ -876,7 +913,7 @@ class FlatZeroOptimizer:
         sd["dynamic_loss_scale"] = self.dynamic_loss_scale
         sd["overflow"] = self.overflow
         sd[CK.CLIP_GRAD] = self.clip_grad
-        sd[CK.PARTITION_COUNT] = self.dp if self.partition else 1
+        sd[CK.PARTITION_COUNT] = self.partition_count()
         sd[CK.BASE_OPTIMIZER_STATE] = self.optimizer.state_dict()
         sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS] = [m.detach().cpu() for m in self.master]
         sd["fp32_host_partitions"] = [m.detach().clone() if m is not None else None for m in self.master_host]
