@@ -423,10 +423,14 @@ class FlatZeroOptimizer:
         # ZeRO-0/1 accumulate locally and reduce only at the accumulation boundary
         return self.is_gradient_accumulation_boundary or self.stage >= 2
 
+    def _local_grads(self):
+        f = getattr(self.optimizer, "skip_grad_allreduce", None)
+        return bool(f()) if f is not None else False
+
     def _div(self):
         # gradient = mean over the GLOBAL batch (dense DP size), for expert groups too; the reference divides expert
         # grads by the expert-DP size only (an ep-times larger scale, `stage_1_and_2.py` average_tensor)
-        return float(self.dp)
+        return 1.0 if self._local_grads() else float(self.dp)
 
     def _prescale(self):
         return self.comm_dtype == torch.float16 and self._div() > 1
@@ -444,7 +448,9 @@ class FlatZeroOptimizer:
             comm = src if src.dtype == self.comm_dtype else src.to(self.comm_dtype)
             if self._prescale():
                 comm.mul_(1.0 / self._div())
-            if g.partition:
+            if self._local_grads():
+                out = comm  # a communication-compressed optimizer (1-bit Adam/LAMB, 0/1 Adam) averages on its own
+            elif g.partition:
                 out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
                 if self.zc is not None and self.zc.zero_quantized_gradients:
                     from .zeropp import quantized_reduce_scatter  # qgZ: int8 all-to-all + fused dequant-reduce
