@@ -83,6 +83,19 @@ class InferenceEngine(torch.nn.Module):
         self.module.eval()
         log_dist(f"InferenceEngine: injected={self.injected} tp={self.tp_size} dtype={self.dtype}", ranks=[0])
 
+    @classmethod
+    def from_ds_model(cls, ds_model: DSInferenceModel, config: DeepSpeedInferenceConfig, tp_group=None, tp_size=1,
+                      tp_rank=0):
+        """Wrap an already-built injected model (hybrid engine, benchmarks) without re-converting weights."""
+        eng = cls.__new__(cls)
+        torch.nn.Module.__init__(eng)
+        eng._config, eng.dtype, eng.injected, eng.module = config, ds_model.dtype, True, ds_model
+        eng.device = ds_model.device if ds_model.device is not None else torch.device("cpu")
+        eng._graphs, eng.cuda_graph_created, eng.model_profile_enabled, eng._model_times = {}, False, False, []
+        eng.tp_size, eng.tp_rank, eng.mp_group, eng.mpu = tp_size, tp_rank, tp_group, None
+        eng.injection_dict = None
+        return eng
+
     # ------------------------------------------------------------------------------------------ groups
     def _create_model_parallel_group(self, config):
         if self.mpu is not None:

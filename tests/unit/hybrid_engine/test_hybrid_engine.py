@@ -1,0 +1,91 @@
+"""Hybrid engine (reference `tests/hybrid_engine/hybrid_engine_test.py`, `tests/unit/hybrid_engine/*`): train with
+ZeRO and generate with the injected inference model on the same (updated) weights; LoRA fuse/unfuse round trip."""
+import copy
+
+import pytest
+import torch
+
+from ..common import run_distributed
+
+transformers = pytest.importorskip("transformers")
+
+
+def _hf_llama():
+    torch.manual_seed(0)
+    c = transformers.LlamaConfig(vocab_size=128, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                 num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
+    return transformers.LlamaForCausalLM(c)
+
+
+class LoRALinear(torch.nn.Module):
+    """DeepSpeed-Chat style LoRA linear with fuse/unfuse."""
+
+    def __init__(self, base, r=4, scale=0.5):
+        super().__init__()
+        self.weight = base.weight
+        self.bias = base.bias
+        self.lora_right_weight = torch.nn.Parameter(torch.randn(base.in_features, r) * 0.1)
+        self.lora_left_weight = torch.nn.Parameter(torch.randn(r, base.out_features) * 0.1)
+        self.lora_scaling = scale
+        self.fused = False
+
+    def fuse_lora_weight(self):
+        self.weight.data += self.lora_scaling * (self.lora_right_weight @ self.lora_left_weight).t()
+        self.fused = True
+
+    def unfuse_lora_weight(self):
+        self.weight.data -= self.lora_scaling * (self.lora_right_weight @ self.lora_left_weight).t()
+        self.fused = False
+
+    def forward(self, x):
+        y = torch.nn.functional.linear(x, self.weight, self.bias)
+        if not self.fused:
+            y = y + self.lora_scaling * (x @ self.lora_right_weight @ self.lora_left_weight)
+        return y
+
+
+def _run(stage, lora, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.runtime.zero.partition_parameters import GatheredParameters
+    model = _hf_llama()
+    if lora:
+        for layer in model.model.layers:
+            layer.self_attn.q_proj = LoRALinear(layer.self_attn.q_proj)
+    cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}},
+           "zero_optimization": {"stage": stage}, "hybrid_engine": {"enabled": True, "max_out_tokens": 64}}
+    if lora:
+        cfg["zero_optimization"]["stage"] = 0
+    eng, _, _, _ = ds.initialize(model=model, config=cfg)
+    ids = torch.randint(0, 128, (2, 8), generator=torch.Generator().manual_seed(3))
+    results = []
+    for it in range(2):
+        got = eng.generate(ids, max_new_tokens=5)
+        # oracle: plain HF generate on a copy holding the gathered training weights (LoRA folded in)
+        with GatheredParameters(list(eng.module.parameters())):
+            ref_model = copy.deepcopy(eng.module)
+        if lora:
+            for m in ref_model.modules():
+                if isinstance(m, LoRALinear):
+                    m.fuse_lora_weight()
+        ref = ref_model.generate(ids, max_new_tokens=5, do_sample=False)
+        results.append((got, ref))
+        x = torch.randint(0, 128, (2, 16), generator=torch.Generator().manual_seed(10 + it + dist.get_rank()))
+        loss = eng(input_ids=x, labels=x).loss
+        eng.backward(loss)
+        eng.step()
+    if lora:  # unfuse restored the training weights exactly
+        for m in eng.module.modules():
+            if isinstance(m, LoRALinear):
+                assert not m.fused
+    if dist.get_rank() == 0:
+        torch.save(results, out)
+
+
+@pytest.mark.parametrize("stage,lora", [(3, False), (2, False), (0, True)])
+def test_hybrid_generate_tracks_training(stage, lora, tmp_path):
+    out = str(tmp_path / "h.pt")
+    run_distributed(_run, 2, stage, lora, out)
+    results = torch.load(out, weights_only=True)
+    for got, ref in results:
+        assert torch.equal(got, ref)
