@@ -1,0 +1,82 @@
+"""Sequence / KV-block bookkeeping for the ragged engine (reference `inference/v2/ragged/{ragged_manager.py:19,
+sequence_descriptor.py, blocked_allocator.py}`)."""
+import torch
+
+from ..kv_cache import BlockedAllocator
+
+
+class DSSequenceDescriptor:
+
+    def __init__(self, uid, block_size):
+        self.uid = uid
+        self.seen_tokens = 0
+        self.in_flight_tokens = 0
+        self.blocks = []
+        self.block_size = block_size
+
+    @property
+    def cur_allocated_blocks(self):
+        return len(self.blocks)
+
+    def blocks_needed(self, new_tokens):
+        total = self.seen_tokens + new_tokens
+        return max(0, -(-total // self.block_size) - len(self.blocks))
+
+    def pre_forward(self, n):
+        self.in_flight_tokens = n
+
+    def post_forward(self):
+        self.seen_tokens += self.in_flight_tokens
+        self.in_flight_tokens = 0
+
+
+class PlaceholderSequenceDescriptor(DSSequenceDescriptor):
+
+    def __init__(self, block_size=64):
+        super().__init__(-1, block_size)
+
+
+class DSStateManager:
+
+    def __init__(self, config, num_blocks, block_size):
+        self.config = config
+        self.block_size = block_size
+        self.allocator = BlockedAllocator(num_blocks)
+        self._seqs = {}
+
+    @property
+    def n_tracked_sequences(self):
+        return len(self._seqs)
+
+    @property
+    def free_blocks(self):
+        return self.allocator.free_blocks
+
+    def get_sequence(self, uid):
+        return self._seqs.get(uid)
+
+    def get_or_create_sequence(self, uid):
+        seq = self._seqs.get(uid)
+        if seq is None:
+            if len(self._seqs) >= self.config.max_tracked_sequences:
+                raise RuntimeError("engine is tracking max_tracked_sequences sequences")
+            seq = self._seqs[uid] = DSSequenceDescriptor(uid, self.block_size)
+        return seq
+
+    def allocate_blocks(self, seq, n_tokens):
+        need = seq.blocks_needed(n_tokens)
+        if need:
+            seq.blocks.extend(self.allocator.allocate(need))
+
+    def flush_sequence(self, uid):
+        seq = self._seqs.pop(uid, None)
+        if seq is not None:
+            self.allocator.free(seq.blocks)
+            seq.blocks = []
+
+    def block_table(self, seqs, device):
+        width = max(len(s.blocks) for s in seqs)
+        bt = torch.zeros(len(seqs), width, dtype=torch.int32)
+        for i, s in enumerate(seqs):
+            bt[i, :len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+        return bt.to(device)
