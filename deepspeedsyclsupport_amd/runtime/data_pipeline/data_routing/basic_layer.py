@@ -1,0 +1,75 @@
+"""Random layerwise token dropping (reference `runtime/data_pipeline/data_routing/basic_layer.py` +
+`csrc/random_ltd/{token_sort.cu, gather_scatter.cu}`).
+
+During training each wrapped layer processes only a random subset of `current_seq` tokens per sample (kept in
+their original order), the rest bypass it unchanged; at eval every token goes through. Gather / scatter along the
+sequence dimension are device index ops (one kernel each), the sorted random subset comes from a single
+`topk` over random keys per sample.
+"""
+import torch
+import torch.nn as nn
+
+
+def token_sort_(indices):
+    return torch.sort(indices, dim=-1).values
+
+
+def token_gather(x, idx, batch_first=True):
+    """x [B, S, H] (or [S, B, H]) -> [B, k, H] keeping positions idx [B, k]."""
+    if not batch_first:
+        x = x.transpose(0, 1)
+    out = torch.gather(x, 1, idx.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
+    return out if batch_first else out.transpose(0, 1)
+
+
+def token_scatter_(full, part, idx, batch_first=True):
+    """full[b, idx[b, j]] = part[b, j] (in place); returns full."""
+    if not batch_first:
+        full_v, part_v = full.transpose(0, 1), part.transpose(0, 1)
+    else:
+        full_v, part_v = full, part
+    full_v.scatter_(1, idx.unsqueeze(-1).expand(-1, -1, full_v.shape[-1]), part_v)
+    return full
+
+
+class RandomLayerTokenDrop(nn.Module):
+
+    def __init__(self, layer, batch_first=True):
+        super().__init__()
+        self.random_ltd_layer = layer
+        self.batch_first = batch_first
+        self.reserved_length = None
+        self.random_ltd_scheduler = None
+        self.random_ltd_num_layer = None
+        self.random_ltd_initialized = False
+
+    def init_config(self, config, scheduler, random_ltd_layer_id):
+        self.random_ltd_scheduler = scheduler
+        self.random_ltd_layer_id = random_ltd_layer_id
+        self.random_ltd_initialized = True
+
+    def forward(self, hidden_states, *args, **kwargs):
+        if self.random_ltd_scheduler is not None:
+            self.reserved_length = self.random_ltd_scheduler.get_current_seq()
+        S = hidden_states.shape[1 if self.batch_first else 0]
+        if not self.training or self.reserved_length is None or self.reserved_length >= S:
+            return self.random_ltd_layer(hidden_states, *args, **kwargs)
+        B = hidden_states.shape[0 if self.batch_first else 1]
+        keys = torch.rand(B, S, device=hidden_states.device)
+        idx = token_sort_(torch.topk(keys, self.reserved_length, dim=-1).indices)
+        part = token_gather(hidden_states, idx, self.batch_first)
+        out = self.random_ltd_layer(part, *args, **kwargs)
+        rest = out[1:] if isinstance(out, tuple) else None
+        out = out[0] if isinstance(out, tuple) else out
+        full = token_scatter_(hidden_states.clone(), out, idx, self.batch_first)
+        return (full, ) + tuple(rest) if rest is not None else full
+
+
+def convert_to_random_ltd(model, layer_cls):
+    """Wrap every instance of `layer_cls` in `model` with RandomLayerTokenDrop (reference helper)."""
+    for name, child in list(model.named_children()):
+        if isinstance(child, layer_cls):
+            setattr(model, name, RandomLayerTokenDrop(child))
+        else:
+            convert_to_random_ltd(child, layer_cls)
+    return model

@@ -1,0 +1,77 @@
+"""Curriculum data sampler (reference `runtime/data_pipeline/data_sampling/data_sampler.py`).
+
+Each sample has a difficulty metric value (e.g. sequence length or vocabulary rarity, precomputed by an analyzer
+and stored as a numpy array / memmap). At every step the sampler draws the global batch only from samples whose
+metric is <= the scheduler's current difficulty (`value` clustering) or from the easiest `difficulty` percentile
+(`percentile`), shuffled with a seed shared by all ranks, and hands each data-parallel rank its slice.
+"""
+import numpy as np
+
+from ..curriculum_scheduler import CurriculumScheduler
+
+
+class DeepSpeedDataSampler:
+
+    def __init__(self, data_efficiency_config, one_epoch_total_samples, micro_batch_size, data_parallel_rank,
+                 data_parallel_size, gradient_accumulation_steps=1, global_rank=0, drop_last=True,
+                 metric_values=None):
+        self.cfg = data_efficiency_config
+        cl = self.cfg.get("data_sampling", {}).get("curriculum_learning", {})
+        self.total = int(one_epoch_total_samples)
+        self.mb = micro_batch_size
+        self.dp_rank, self.dp_size = data_parallel_rank, data_parallel_size
+        self.gas = gradient_accumulation_steps
+        self.global_batch = micro_batch_size * data_parallel_size * gradient_accumulation_steps
+        self.seed = int(self.cfg.get("seed", 1234))
+        self.metrics = {}
+        self.schedulers = {}
+        for name, mc in cl.get("curriculum_metrics", {}).items():
+            self.schedulers[name] = CurriculumScheduler(mc)
+            vals = metric_values.get(name) if metric_values else None
+            if vals is None and mc.get("sample_to_metric_path"):
+                vals = np.load(mc["sample_to_metric_path"], mmap_mode="r")  # numpy, allow_pickle=False
+            self.metrics[name] = (np.asarray(vals), mc.get("difficulty_type", "value"))
+        self.consumed_samples = 0
+        self.curriculum_step = 0
+        self.np_rng = np.random.default_rng(self.seed)
+
+    def __len__(self):
+        return self.total
+
+    def _eligible(self):
+        mask = np.ones(self.total, dtype=bool)
+        for name, (vals, dtype) in self.metrics.items():
+            d = self.schedulers[name].update_difficulty(self.curriculum_step)
+            if dtype == "percentile":
+                thr = np.percentile(vals, d)
+                mask &= vals <= thr
+            else:
+                mask &= vals <= d
+        idx = np.nonzero(mask)[0]
+        return idx if idx.size else np.arange(self.total)
+
+    def get_next_global_batch(self):
+        self.curriculum_step += 1
+        pool = self._eligible()
+        batch = self.np_rng.choice(pool, size=self.global_batch, replace=pool.size < self.global_batch)
+        self.consumed_samples += self.global_batch
+        return batch
+
+    def __iter__(self):
+        while self.consumed_samples < self.total:
+            gb = self.get_next_global_batch()
+            per_rank = gb.reshape(self.gas, self.dp_size, self.mb)[:, self.dp_rank]
+            for micro in per_rank:
+                yield micro.tolist()
+
+    def state_dict(self):
+        return {"consumed_samples": self.consumed_samples, "curriculum_step": self.curriculum_step,
+                "rng": self.np_rng.bit_generator.state,
+                "schedulers": {k: s.get_state() for k, s in self.schedulers.items()}}
+
+    def load_state_dict(self, sd):
+        self.consumed_samples = sd["consumed_samples"]
+        self.curriculum_step = sd["curriculum_step"]
+        self.np_rng.bit_generator.state = sd["rng"]
+        for k, st in sd["schedulers"].items():
+            self.schedulers[k].set_state(st)

@@ -99,8 +99,38 @@ class DeepSpeedEngine(nn.Module):
             from ..profiling.flops_profiler import FlopsProfiler
             self.flops_profiler = FlopsProfiler(self.module, ds_engine=self)
         self._configure_checkpointing()
+        self._configure_data_efficiency()
         if self._config.print_user_config if hasattr(self._config, "print_user_config") and False else False:
             self._config.print("DeepSpeedEngine configuration")
+
+    # ============================================================================================ data efficiency
+    def _configure_data_efficiency(self):
+        self.curriculum_scheduler_legacy = None
+        self.random_ltd_scheduler = None
+        self.compression_scheduler = None
+        if self._config.curriculum_enabled_legacy:
+            from .data_pipeline.curriculum_scheduler import CurriculumScheduler
+            self.curriculum_scheduler_legacy = CurriculumScheduler(self._config.curriculum_params_legacy)
+        de = self._config.data_efficiency_config or {}
+        rl = de.get("data_routing", {}).get("random_ltd", {})
+        if de.get("enabled", False) and rl.get("enabled", False):
+            from .data_pipeline.data_routing import RandomLayerTokenDrop, RandomLTDScheduler
+            self.random_ltd_scheduler = RandomLTDScheduler(rl)
+            for i, m in enumerate(x for x in self.module.modules() if isinstance(x, RandomLayerTokenDrop)):
+                m.init_config(rl, self.random_ltd_scheduler, i)
+        if self._config.compression_config:
+            from ..compression.compress import compression_scheduler
+            self.compression_scheduler = compression_scheduler(self.module, self._config.compression_config)
+
+    def _module_accepts(self, kw):
+        import inspect
+        try:
+            return kw in inspect.signature(self.module.forward).parameters
+        except (TypeError, ValueError):
+            return False
+
+    def get_data_parallel_rank(self):
+        return dist.get_rank(self.seq_data_parallel_group) if self.seq_data_parallel_group is not None else 0
 
     # ============================================================================================ setup
     def _set_distributed_vars(self, args):
@@ -355,6 +385,11 @@ class DeepSpeedEngine(nn.Module):
         self.timers(FORWARD_MICRO_TIMER).start()
         if self.training and self.optimizer is not None:
             self.optimizer.is_gradient_accumulation_boundary = self.is_gradient_accumulation_boundary()
+        if self.training and self.curriculum_scheduler_legacy is not None:
+            # legacy curriculum (reference engine.py forward): sequence-length difficulty handed to the model
+            d = self.curriculum_scheduler_legacy.update_difficulty(self.global_steps + 1)
+            if self._module_accepts("curriculum_seqlen"):
+                kwargs["curriculum_seqlen"] = d
         loss = self.module(*inputs, **kwargs)
         self.timers(FORWARD_MICRO_TIMER).stop()
         return loss
@@ -403,6 +438,10 @@ class DeepSpeedEngine(nn.Module):
                     self.optimizer.coordinator.reset_step()
             self.global_steps += 1
             self.global_samples += self.train_batch_size()
+            if self.compression_scheduler is not None:
+                self.compression_scheduler.step(self.global_steps)
+            if self.random_ltd_scheduler is not None:
+                self.random_ltd_scheduler.update_seq(self.global_steps)
             if self.flops_profiler is not None and self.flops_profiler.started:
                 self.flops_profiler.stop_profile()
                 self.flops_profiler.print_model_profile(profile_step=self.global_steps)

@@ -1,0 +1,68 @@
+"""Data efficiency (reference `tests/unit/runtime/test_data_efficiency.py`, curriculum scheduler tests)."""
+import numpy as np
+import pytest
+import torch
+
+from deepspeedsyclsupport_amd.runtime.data_pipeline import CurriculumScheduler
+from deepspeedsyclsupport_amd.runtime.data_pipeline.data_routing import RandomLayerTokenDrop, RandomLTDScheduler
+from deepspeedsyclsupport_amd.runtime.data_pipeline.data_sampling import DeepSpeedDataSampler
+
+
+def test_fixed_linear_and_root():
+    c = CurriculumScheduler({"min_difficulty": 8, "max_difficulty": 64, "schedule_type": "fixed_linear",
+                             "schedule_config": {"total_curriculum_step": 10, "difficulty_step": 8}})
+    seq = [c.update_difficulty(s) for s in range(0, 14)]
+    assert seq[0] == 8 and seq[-1] == 64 and all(b >= a for a, b in zip(seq, seq[1:]))
+    assert all(v % 8 == 0 for v in seq)
+    r = CurriculumScheduler({"min_difficulty": 8, "max_difficulty": 64, "schedule_type": "fixed_root",
+                             "schedule_config": {"total_curriculum_step": 10, "difficulty_step": 8,
+                                                 "root_degree": 2}})
+    assert r.get_difficulty(2) >= c.get_difficulty(2)  # root schedules ramp faster early
+
+
+def test_fixed_discrete_and_custom():
+    c = CurriculumScheduler({"min_difficulty": 1, "max_difficulty": 3, "schedule_type": "fixed_discrete",
+                             "schedule_config": {"difficulty": [1, 2, 3], "max_step": [5, 10]}})
+    assert [c.get_difficulty(s) for s in (0, 5, 6, 10, 11, 100)] == [1, 1, 2, 2, 3, 3]
+    cu = CurriculumScheduler({"min_difficulty": 0, "max_difficulty": 10, "schedule_type": "custom"})
+    cu.set_custom_get_difficulty(lambda s: min(s, 10))
+    assert cu.update_difficulty(4) == 4
+    with pytest.raises(AssertionError):
+        CurriculumScheduler({"min_difficulty": 1, "max_difficulty": 3, "schedule_type": "fixed_discrete",
+                             "schedule_config": {"difficulty": [1, 2], "max_step": [5, 10]}})
+
+
+def test_curriculum_sampler_respects_difficulty():
+    vals = np.arange(100)  # difficulty = sample index
+    cfg = {"seed": 3, "data_sampling": {"curriculum_learning": {"curriculum_metrics": {"seqlen": {
+        "min_difficulty": 10, "max_difficulty": 100, "schedule_type": "fixed_linear",
+        "schedule_config": {"total_curriculum_step": 5, "difficulty_step": 10}}}}}}
+    s0 = DeepSpeedDataSampler(cfg, 100, 2, 0, 2, metric_values={"seqlen": vals})
+    first = s0.get_next_global_batch()
+    assert first.max() <= 20
+    later = [s0.get_next_global_batch() for _ in range(6)][-1]
+    assert later.max() > 20
+    # ranks see disjoint slices of the same global batch
+    a = DeepSpeedDataSampler(cfg, 16, 2, 0, 2, metric_values={"seqlen": vals[:16]})
+    b = DeepSpeedDataSampler(cfg, 16, 2, 1, 2, metric_values={"seqlen": vals[:16]})
+    ia, ib = next(iter(a)), next(iter(b))
+    assert len(ia) == 2 and len(ib) == 2 and not set(ia) & set(ib)
+
+
+def test_random_ltd_layer():
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(8, 8)
+    layer = RandomLayerTokenDrop(lin)
+    sch = RandomLTDScheduler({"random_ltd_schedule": {"min_value": 4, "max_value": 16,
+                                                      "schedule_config": {"require_steps": 4, "seq_per_step": 4}}})
+    layer.init_config({}, sch, 0)
+    x = torch.randn(2, 16, 8)
+    y = layer(x)
+    changed = (y != x).any(-1)
+    assert changed.sum(1).tolist() == [4, 4]  # exactly the kept tokens went through the layer
+    sch.update_seq(4)
+    assert sch.get_current_seq() == 16
+    torch.testing.assert_close(layer(x), lin(x))
+    layer.eval()
+    sch.set_current_seq(4)
+    torch.testing.assert_close(layer(x), lin(x))
