@@ -1,0 +1,3 @@
+"""ZeRO-Infinity NVMe swapping (reference `runtime/swap_tensor/`)."""
+from .optimizer_swapper import OptimizerStateSwapper
+from .tensor_swapper import AsyncTensorSwapper

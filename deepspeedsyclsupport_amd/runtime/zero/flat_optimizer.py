@@ -148,6 +148,15 @@ class FlatZeroOptimizer:
             self.offload = True
             self.offload_ratio = float(self.zc.offload_optimizer.ratio)
             self.offload_pin = bool(self.zc.offload_optimizer.pin_memory)
+        self.nvme_swapper = None
+        if self.offload and str(getattr(self.zc.offload_optimizer.device, "value",
+                                        self.zc.offload_optimizer.device)) == "nvme":
+            import os
+            from ..swap_tensor import OptimizerStateSwapper
+            path = self.zc.offload_optimizer.nvme_path or "/tmp/ds_nvme_swap"
+            folder = os.path.join(path, f"zero_stage_{self.stage}", "optimizer", f"rank{dist.get_rank()}")
+            self.nvme_swapper = OptimizerStateSwapper(ds_config.aio_config, folder,
+                                                      pin=self.device.type == "cuda")
         # fp16 loss scaling
         fp16 = dtype == torch.float16
         self.loss_scaler = CreateLossScaler(dtype, getattr(ds_config, "loss_scale", 0) or 1.0,
@@ -731,19 +740,32 @@ class FlatZeroOptimizer:
             hp = self.master_host[og]
             if hp is None:
                 continue
-            st = self.host_states.get(og)
-            if st is None:
-                st = [torch.zeros_like(hp), torch.zeros_like(hp), 0]
-                self.host_states[og] = st
-            st[2] += 1
             b1, b2 = group["betas"]
             lp = self._host_lp.get(og)
             if lp is None:
                 lp = torch.empty(hp.numel(), dtype=self.dtype, pin_memory=self.device.type == "cuda")
                 self._host_lp[og] = lp
-            cpu_ops().cpu_adam_update(hp, st[0], st[1], self.grad_acc_host[og], lp, st[2], group["lr"], b1, b2,
-                                      group["eps"], group["weight_decay"], group.get("bias_correction", True),
-                                      bool(getattr(self.optimizer, "adam_w_mode", True)), grad_scale)
+            adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+            bc = group.get("bias_correction", True)
+            gr = self.grad_acc_host[og]
+            if self.nvme_swapper is not None:
+                # ZeRO-Infinity: moments stream from NVMe chunk by chunk (read-ahead / write-behind)
+                if og not in self.nvme_swapper.sizes:
+                    self.nvme_swapper.register(og, hp.numel())
+
+                def upd(lo, hi, m, v, step, hp=hp, lp=lp, gr=gr, group=group, b1=b1, b2=b2):
+                    cpu_ops().cpu_adam_update(hp[lo:hi], m, v, gr[lo:hi], lp[lo:hi], step, group["lr"], b1, b2,
+                                              group["eps"], group["weight_decay"], bc, adamw, grad_scale)
+
+                self.nvme_swapper.step(og, upd)
+                continue
+            st = self.host_states.get(og)
+            if st is None:
+                st = [torch.zeros_like(hp), torch.zeros_like(hp), 0]
+                self.host_states[og] = st
+            st[2] += 1
+            cpu_ops().cpu_adam_update(hp, st[0], st[1], gr, lp, st[2], group["lr"], b1, b2, group["eps"],
+                                      group["weight_decay"], bc, adamw, grad_scale)
 
     def _host_writeback(self):
         for g in self.groups:
@@ -804,6 +826,8 @@ class FlatZeroOptimizer:
             if key == "fp32":
                 return (self.master_host if on_host else self.master)[og]
             if on_host:
+                if self.nvme_swapper is not None and og in self.nvme_swapper.sizes:
+                    return self.nvme_swapper.read_full(og)[self._STATE_IDX[key]]
                 st = self.host_states.get(og)
                 return None if st is None else st[self._STATE_IDX[key]]
             st = self.optimizer.state.get(self.fp32_flat[og], {})
@@ -924,6 +948,10 @@ class FlatZeroOptimizer:
         sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS] = [m.detach().cpu() for m in self.master]
         sd["fp32_host_partitions"] = [m.detach().clone() if m is not None else None for m in self.master_host]
         sd["host_optimizer_states"] = {og: [s[0].clone(), s[1].clone(), s[2]] for og, s in self.host_states.items()}
+        if self.nvme_swapper is not None:
+            for og in self.nvme_swapper.sizes:
+                m, v, st = self.nvme_swapper.read_full(og)
+                sd["host_optimizer_states"][og] = [m, v, st]
         sd[CK.FLAT_LAYOUT] = self.layout()
         sd[CK.DS_VERSION] = _version()
         return sd
@@ -946,7 +974,12 @@ class FlatZeroOptimizer:
                     for k, v in st.items()
                 }
             for og, s in sd.get("host_optimizer_states", {}).items():
-                self.host_states[int(og)] = [s[0].clone(), s[1].clone(), s[2]]
+                if self.nvme_swapper is not None:
+                    if int(og) not in self.nvme_swapper.sizes:
+                        self.nvme_swapper.register(int(og), s[0].numel())
+                    self.nvme_swapper.write_full(int(og), s[0], s[1], s[2])
+                else:
+                    self.host_states[int(og)] = [s[0].clone(), s[1].clone(), s[2]]
         if CK.LOSS_SCALER in sd:
             ls = sd[CK.LOSS_SCALER]
             if isinstance(ls, dict):
