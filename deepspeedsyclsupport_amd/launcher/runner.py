@@ -177,6 +177,20 @@ def main(args=None):
         raise RuntimeError("no resources left after include/exclude filtering")
     if not args.master_addr:
         args.master_addr = next(iter(active)) if multi else "127.0.0.1"
+    if args.autotuning:
+        from ..autotuning import Autotuner
+        tuner = Autotuner(args, active)
+        best = tuner.tune()
+        tuner.print_tuning_results()
+        if args.autotuning == "tune" or best is None:
+            return 0
+        # "run": launch the user script with the optimal config
+        opt_cfg = os.path.join(tuner.results_dir, "ds_config_optimal.json")
+        ua = list(args.user_args)
+        if "--deepspeed_config" in ua:
+            ua[ua.index("--deepspeed_config") + 1] = opt_cfg
+        args.user_args = ua
+        args.autotuning = ""
     world_info = encode_world_info(active)
     multi_node = args.force_multi or len(active) > 1
     if args.elastic_training:

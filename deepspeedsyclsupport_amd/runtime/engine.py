@@ -100,6 +100,7 @@ class DeepSpeedEngine(nn.Module):
             self.flops_profiler = FlopsProfiler(self.module, ds_engine=self)
         self._configure_checkpointing()
         self._configure_data_efficiency()
+        self._configure_autotuning()
         if self._config.print_user_config if hasattr(self._config, "print_user_config") and False else False:
             self._config.print("DeepSpeedEngine configuration")
 
@@ -121,6 +122,49 @@ class DeepSpeedEngine(nn.Module):
         if self._config.compression_config:
             from ..compression.compress import compression_scheduler
             self.compression_scheduler = compression_scheduler(self.module, self._config.compression_config)
+
+    def _configure_autotuning(self):
+        """Autotuning experiment mode (reference engine.py autotuning hooks): report model info, or measure the
+        metric between start_profile_step and end_profile_step, write it to metric_path, and end the process."""
+        at = (self._config.autotuning_config or {})
+        self._autotuning = at if at.get("enabled", False) and (at.get("metric_path") or
+                                                              at.get("model_info", {}).get("profile")) else None
+        self._at_t0 = None
+        if self._autotuning is not None and at.get("model_info", {}).get("profile"):
+            import json
+            n = sum(p.numel() for p in self.module.parameters())
+            path = at.get("model_info_path")
+            if self.global_rank == 0 and path:
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                with open(path, "w") as f:
+                    json.dump({"num_params": n}, f)
+            if at.get("metric_path") and self.global_rank == 0:
+                os.makedirs(os.path.dirname(at["metric_path"]), exist_ok=True)
+                with open(at["metric_path"], "w") as f:
+                    json.dump({"num_params": n}, f)
+            dist.barrier()
+            raise SystemExit(0)
+
+    def _autotuning_step(self):
+        import json
+        import time
+        at = self._autotuning
+        start, end = at.get("start_profile_step", 3), at.get("end_profile_step", 5)
+        if self.global_steps == start:
+            self.acc.synchronize()
+            self._at_t0 = time.time()
+        elif self.global_steps == end and self._at_t0 is not None:
+            self.acc.synchronize()
+            dt = (time.time() - self._at_t0) / max(end - start, 1)
+            res = {"throughput": self.train_batch_size() / dt, "latency": dt,
+                   "flops": None, "micro_batch": self.train_micro_batch_size_per_gpu(),
+                   "zero_stage": self.zero_optimization_stage()}
+            if self.global_rank == 0:
+                os.makedirs(os.path.dirname(at["metric_path"]) or ".", exist_ok=True)
+                with open(at["metric_path"], "w") as f:
+                    json.dump(res, f)
+            dist.barrier()
+            raise SystemExit(0)
 
     def _module_accepts(self, kw):
         import inspect
@@ -440,6 +484,8 @@ class DeepSpeedEngine(nn.Module):
             self.global_samples += self.train_batch_size()
             if self.compression_scheduler is not None:
                 self.compression_scheduler.step(self.global_steps)
+            if self._autotuning is not None:
+                self._autotuning_step()
             if self.random_ltd_scheduler is not None:
                 self.random_ltd_scheduler.update_seq(self.global_steps)
             if self.flops_profiler is not None and self.flops_profiler.started:
