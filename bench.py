@@ -38,6 +38,41 @@ def parse():
     return ap.parse_args()
 
 
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "tunableop_llama7b_gfx950.csv")
+
+
+def setup_gemm_tuning(on_gpu):
+    """hipBLASLt/rocBLAS solution selection via PyTorch TunableOp. `DS_BENCH_TUNABLEOP=tune` measures every
+    candidate solution for each GEMM shape of the step and records the winners in profiles/ (done once per
+    model/config on an MI355X); the default `use` replays that table (no tuning inside the timed region)."""
+    mode = os.environ.get("DS_BENCH_TUNABLEOP", "use")
+    if not on_gpu or mode == "off":
+        return
+    tun = torch.cuda.tunable
+    if mode == "tune":
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_max_tuning_duration(int(os.environ.get("DS_TUNABLEOP_MS", "30")))
+        tun.set_max_tuning_iterations(int(os.environ.get("DS_TUNABLEOP_ITERS", "20")))
+        tun.set_filename(TUNED_GEMMS, False)
+        log(f"[bench] TunableOp tuning -> {TUNED_GEMMS}")
+        import threading
+
+        def heartbeat():  # tuning a step's GEMM shapes takes minutes: keep the job visibly alive
+            t0 = time.time()
+            while True:
+                time.sleep(30)
+                log(f"[bench] tuning... {time.time() - t0:.0f}s, {len(tun.get_results())} shapes done")
+
+        threading.Thread(target=heartbeat, daemon=True).start()
+    elif os.path.exists(TUNED_GEMMS):
+        tun.enable(True)
+        tun.tuning_enable(False)
+        tun.set_filename(TUNED_GEMMS, False)
+        tun.read_file(TUNED_GEMMS)
+        log(f"[bench] TunableOp replaying {TUNED_GEMMS}")
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -59,6 +94,7 @@ def main():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     on_gpu = dev.type == "cuda"
+    setup_gemm_tuning(on_gpu)
 
     def sync():
         if on_gpu:
