@@ -53,3 +53,18 @@ def test_sparse_allreduce(tmp_path):
     run_distributed(_sparse, 2, out)
     d = torch.load(out, weights_only=True)
     torch.testing.assert_close(d["got"], d["ref"])
+
+
+def test_partition_balanced_and_norms():
+    from deepspeedsyclsupport_amd.runtime.utils import (clip_grad_norm_, get_global_norm_of_tensors,
+                                                        partition_balanced, partition_uniform)
+    assert partition_uniform(10, 3) == [0, 4, 7, 10]
+    parts = partition_balanced([1, 1, 1, 10, 1, 1, 1, 1], 3)
+    sizes = [sum([1, 1, 1, 10, 1, 1, 1, 1][a:b]) for a, b in zip(parts, parts[1:])]
+    assert parts[0] == 0 and parts[-1] == 8 and max(sizes) == 10
+    ps = [torch.nn.Parameter(torch.ones(4)) for _ in range(2)]
+    for p in ps:
+        p.grad = torch.full((4, ), 3.0)
+    n = clip_grad_norm_(ps, 1.0)
+    assert abs(n - math.sqrt(8 * 9)) < 1e-5
+    assert abs(get_global_norm_of_tensors([p.grad for p in ps]) - 1.0) < 1e-4
