@@ -618,7 +618,13 @@ class DeepSpeedEngine(nn.Module):
             path = os.path.join(load_dir, str(tag), f"{CK.ZERO_FILE_PREFIX}0_mp_rank_00{CK.MODEL_FILE_SUFFIX}")
         ck = self.checkpoint_engine.load(path, map_location="cpu")
         self._load_module_state(ck["module"], strict=load_module_strict)
-        if not load_module_only and self.optimizer is not None:
+        universal = bool(self._config.checkpoint_config.get("load_universal", False)) \
+            if isinstance(self._config.checkpoint_config, dict) else \
+            bool(getattr(self._config.checkpoint_config, "load_universal", False))
+        if universal and not load_module_only and self.optimizer is not None:
+            from ..checkpoint.ds_to_universal import load_universal_into
+            load_universal_into(self.optimizer, self.module, os.path.join(load_dir, str(tag)))
+        elif not load_module_only and self.optimizer is not None:
             zpath = self._get_zero_ckpt_name(load_dir, tag)
             if os.path.exists(zpath):
                 zsd = self.checkpoint_engine.load(zpath, map_location="cpu")

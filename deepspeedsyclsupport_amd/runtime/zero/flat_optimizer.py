@@ -882,6 +882,27 @@ class FlatZeroOptimizer:
         """Gather the fp32 master value of one parameter (reference `safe_get_full_fp32_param`)."""
         return self._gather_param(p, self._state_src("fp32"))
 
+    def _ensure_state(self, key=None):
+        """Materialise (zero) Adam moments for every optimizer group so they can be written into."""
+        for og in range(len(self.fp32_flat)):
+            fp = self.fp32_flat[og]
+            st = self.optimizer.state[fp]
+            if len(st) == 0:
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros_like(fp.data)
+                st["exp_avg_sq"] = torch.zeros_like(fp.data)
+            hp = self.master_host[og] if og < len(self.master_host) else None
+            if hp is not None and self.nvme_swapper is None and og not in self.host_states:
+                self.host_states[og] = [torch.zeros_like(hp), torch.zeros_like(hp), 0]
+
+    def set_step(self, step):
+        for og in range(len(self.fp32_flat)):
+            st = self.optimizer.state[self.fp32_flat[og]]
+            if "step" in st:
+                st["step"] = int(step)
+        for st in self.host_states.values():
+            st[2] = int(step)
+
     def get_full_optimizer_state(self, p, key):
         return self._gather_param(p, self._state_src(key))
 

@@ -64,27 +64,52 @@ def _resolve(checkpoint_dir, tag):
     return path
 
 
-def _get_fp32_state_dict_from_zero_checkpoint(ds_checkpoint_dir, exclude_frozen_parameters=False):
-    files = get_optim_files(ds_checkpoint_dir)
-    states = [_load(f)[OPTIMIZER_STATE_DICT] for f in files]
+def _flat_source(st, key):
+    """fetch(og, on_host) -> the rank's flat fp32 tensor holding `key` (fp32 master or an Adam moment)."""
+    masters = st[SINGLE_PARTITION_OF_FP32_GROUPS]
+    host = st.get("fp32_host_partitions") or []
+    base = st.get("base_optimizer_state") or {}
+    host_states = st.get("host_optimizer_states") or {}
+    idx = {"exp_avg": 0, "exp_avg_sq": 1}
+
+    def fetch(og, on_host):
+        if key == "fp32":
+            return host[og] if on_host else masters[og]
+        if on_host:
+            hs = host_states.get(og, host_states.get(str(og)))
+            return None if hs is None else hs[idx[key]]
+        pid = base["param_groups"][og]["params"][0]
+        return base["state"].get(pid, {}).get(key)
+
+    return fetch
+
+
+def _reassemble(states, key):
     layout0 = states[0][FLAT_LAYOUT]
     out = OrderedDict()
     for gi, g in enumerate(layout0):
         full = torch.zeros(g["padded"], dtype=torch.float32)
-        if g["partition"]:
-            owners = range(len(states))
-        else:
-            owners = [0]  # replicated group: every rank holds the whole segment
+        owners = range(len(states)) if g["partition"] else [0]
         for r in owners:
             st = states[r]
             lg = st[FLAT_LAYOUT][gi]
-            masters = st[SINGLE_PARTITION_OF_FP32_GROUPS]
-            host = st.get("fp32_host_partitions") or []
+            fetch = _flat_source(st, key)
             for (s, e, og, moff, on_host) in lg["runs"]:
-                src = host[og] if on_host else masters[og]
-                full[lg["seg_lo"] + s:lg["seg_lo"] + e] = src[moff:moff + e - s].float()
+                src = fetch(og, on_host)
+                if src is not None:
+                    full[lg["seg_lo"] + s:lg["seg_lo"] + e] = src[moff:moff + e - s].float()
         for name, shape, off, numel in g["params"]:
             out[name] = full[off:off + numel].view(shape).clone()
+    return out
+
+
+def load_optim_states(ds_checkpoint_dir):
+    return [_load(f)[OPTIMIZER_STATE_DICT] for f in get_optim_files(ds_checkpoint_dir)]
+
+
+def _get_fp32_state_dict_from_zero_checkpoint(ds_checkpoint_dir, exclude_frozen_parameters=False):
+    states = load_optim_states(ds_checkpoint_dir)
+    out = _reassemble(states, "fp32")
     # buffers (and any non-partitioned tensors) come from the 16-bit model file
     try:
         model_sd = _load(get_model_state_file(ds_checkpoint_dir))

@@ -122,3 +122,41 @@ def _tag_mismatch(ckpt):
 
 def test_tag_validation_fail(tmp_path):
     run_distributed(_tag_mismatch, 2, str(tmp_path / "c"))
+
+
+def _universal_src(ckpt, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.utils import safe_get_full_fp32_param, safe_get_full_optimizer_state
+    eng, _, _, _ = ds.initialize(model=tiny_llama(), config=_cfg(3, "fp32"))
+    _train(eng, random_tokens(2, 2, 16, seed=21 + dist.get_rank()), 2)
+    eng.save_checkpoint(ckpt, tag="u")
+    ref = {n: (safe_get_full_fp32_param(p), safe_get_full_optimizer_state(p, "exp_avg"),
+               safe_get_full_optimizer_state(p, "exp_avg_sq")) for n, p in eng.module.named_parameters()}
+    if dist.get_rank() == 0:
+        torch.save(ref, out)
+
+
+def _universal_dst(ckpt, ref_path):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd.utils import safe_get_full_fp32_param, safe_get_full_optimizer_state
+    c = _cfg(1, "fp32")
+    c["checkpoint"] = {"load_universal": True}
+    eng, _, _, _ = ds.initialize(model=tiny_llama(seed=7), config=c)
+    eng.load_checkpoint(ckpt, tag="u_universal")
+    ref = torch.load(ref_path, weights_only=True)
+    for n, p in eng.module.named_parameters():
+        torch.testing.assert_close(safe_get_full_fp32_param(p), ref[n][0], rtol=0, atol=0, msg=n)
+        torch.testing.assert_close(safe_get_full_optimizer_state(p, "exp_avg"), ref[n][1], rtol=0, atol=0)
+        torch.testing.assert_close(safe_get_full_optimizer_state(p, "exp_avg_sq"), ref[n][2], rtol=0, atol=0)
+    assert eng.global_steps == 2
+    _train(eng, random_tokens(1, 2, 16, seed=99), 1)  # and training continues
+
+
+def test_universal_checkpoint_changes_topology(tmp_path):
+    """ZeRO-3 on 2 ranks -> universal -> ZeRO-1 on 3 ranks with every fp32 master and moment intact."""
+    from deepspeedsyclsupport_amd.checkpoint.ds_to_universal import ds_to_universal
+    ckpt, ref = str(tmp_path / "ck"), str(tmp_path / "ref.pt")
+    run_distributed(_universal_src, 2, ckpt, ref)
+    ds_to_universal(os.path.join(ckpt, "u"), os.path.join(ckpt, "u_universal"))
+    run_distributed(_universal_dst, 3, ckpt, ref)
