@@ -201,7 +201,7 @@ class InferenceEngine(torch.nn.Module):
         """One decode step for every sequence (ids [B, 1]); uses a captured HIP graph when enabled."""
         B = ids.shape[0]
         graphable = (self._config.enable_cuda_graph and self.device.type == "cuda" and self.dtype == torch.bfloat16
-                     and self.module.spec.head_dim in (64, 128, 256))
+                     and self.module.spec.head_dim in (64, 128, 256) and not self.module.spec.num_experts)
         if not graphable:  # the gather-based fallback attention syncs with the host and cannot be captured
             meta = self._meta(bt, lens, 1, max_len)
             return self.module(ids, meta)

@@ -208,9 +208,131 @@ def _gptj(model):
     return spec, top, layers
 
 
+def _mixtral(model):
+    """Mixtral / Qwen2-MoE style sparse MLP (reference v2 `model_implementations/mixtral/`): the llama attention
+    stack plus a top-k router over gated experts; HF keeps the experts fused as `gate_up_proj` [E, 2I, H] and
+    `down_proj` [E, H, I]."""
+    cfg = model.config
+    spec, top, _ = _llama_like_spec_only(model)
+    spec.arch = "mixtral"
+    spec.num_experts = cfg.num_local_experts
+    spec.moe_top_k = cfg.num_experts_per_tok
+    base = model.model
+    layers = []
+    for L in base.layers:
+        a, m = L.self_attn, L.mlp
+        ex = m.experts
+        layers.append(dict(ln1_w=L.input_layernorm.weight, ln2_w=L.post_attention_layernorm.weight,
+                           q_w=a.q_proj.weight, k_w=a.k_proj.weight, v_w=a.v_proj.weight, o_w=a.o_proj.weight,
+                           router_w=m.gate.weight, experts_gate_up=ex.gate_up_proj, experts_down=ex.down_proj))
+    return spec, top, layers
+
+
+def _llama_like_spec_only(model):
+    cfg = model.config
+    theta, partial = _rope(cfg)
+    nh = cfg.num_attention_heads
+    hd = getattr(cfg, "head_dim", None) or cfg.hidden_size // nh
+    spec = DSModelSpec(arch=cfg.model_type, vocab_size=cfg.vocab_size, hidden_size=cfg.hidden_size,
+                       num_layers=cfg.num_hidden_layers, num_heads=nh,
+                       num_kv_heads=getattr(cfg, "num_key_value_heads", None) or nh,
+                       intermediate_size=cfg.intermediate_size, head_dim=hd, norm="rms", norm_eps=cfg.rms_norm_eps,
+                       pos="rope", rope_theta=theta, rotary_dim=int(hd * partial), act=cfg.hidden_act,
+                       gated_mlp=True, max_positions=cfg.max_position_embeddings,
+                       sliding_window=getattr(cfg, "sliding_window", None) or 0,
+                       tie_embeddings=bool(getattr(cfg, "tie_word_embeddings", False)))
+    top = dict(embed=model.model.embed_tokens.weight, norm_w=model.model.norm.weight, lm_head=model.lm_head.weight)
+    return spec, top, None
+
+
+def _falcon(model):
+    """Falcon 7B/40B/180B (reference `module_inject/containers` has no Falcon policy; v2 `model_implementations/
+    falcon/`): fused query_key_value in one of three layouts, parallel attention+MLP with one shared or two
+    separate LayerNorms, multi-query / grouped KV heads, rotary positions, bias-free GELU MLP."""
+    cfg = model.config
+    H, nh = cfg.hidden_size, cfg.num_attention_heads
+    hd = H // nh
+    assert not cfg.alibi, "ALiBi Falcon variants are not supported by the injected kernels"
+    new = bool(cfg.new_decoder_architecture)
+    nk = cfg.num_kv_heads if new else (1 if cfg.multi_query else nh)
+    n_ln = (cfg.num_ln_in_parallel_attn or 2) if new else 1
+    assert cfg.parallel_attn or not new, "sequential attention with the new decoder layout is not a Falcon model"
+    theta, _ = _rope(cfg)
+    spec = DSModelSpec(arch="falcon", vocab_size=cfg.vocab_size, hidden_size=H, num_layers=cfg.num_hidden_layers,
+                       num_heads=nh, num_kv_heads=nk, intermediate_size=getattr(cfg, "ffn_hidden_size", None) or 4 * H,
+                       norm="ln", norm_eps=cfg.layer_norm_epsilon, pos="rope", rope_theta=theta, act="gelu",
+                       gated_mlp=False, qkv_bias=cfg.bias, o_bias=cfg.bias, mlp_bias=cfg.bias,
+                       parallel_residual=bool(cfg.parallel_attn),
+                       shared_parallel_norm=bool(cfg.parallel_attn) and n_ln == 1,
+                       max_positions=cfg.max_position_embeddings,
+                       tie_embeddings=bool(getattr(cfg, "tie_word_embeddings", True)))
+
+    def split(w):
+        if w is None:
+            return None, None, None
+        shp = w.shape[1:]
+        if new:
+            g = w.reshape(nk, nh // nk + 2, hd, *shp)
+            return g[:, :-2].reshape(nh * hd, *shp), g[:, -2].reshape(nk * hd, *shp), g[:, -1].reshape(nk * hd, *shp)
+        if cfg.multi_query:
+            return w.split([nh * hd, hd, hd], 0)
+        return _split_interleaved(w, nh, hd)
+
+    tr = model.transformer
+    layers = []
+    for L in tr.h:
+        sa, mlp = L.self_attention, L.mlp
+        q, k, v = split(sa.query_key_value.weight)
+        qb, kb, vb = split(_t(sa.query_key_value.bias))
+        if n_ln == 2:
+            n1, n2 = L.ln_attn, L.ln_mlp
+        else:
+            n1 = L.input_layernorm
+            n2 = getattr(L, "post_attention_layernorm", None) if not cfg.parallel_attn else None
+        lw = dict(ln1_w=n1.weight, ln1_b=n1.bias, q_w=q, k_w=k, v_w=v, q_b=qb, k_b=kb, v_b=vb,
+                  o_w=sa.dense.weight, o_b=_t(sa.dense.bias), fc1_w=mlp.dense_h_to_4h.weight,
+                  fc1_b=_t(mlp.dense_h_to_4h.bias), fc2_w=mlp.dense_4h_to_h.weight, fc2_b=_t(mlp.dense_4h_to_h.bias))
+        if n2 is not None:
+            lw.update(ln2_w=n2.weight, ln2_b=n2.bias)
+        layers.append(lw)
+    top = dict(embed=tr.word_embeddings.weight, norm_w=tr.ln_f.weight, norm_b=tr.ln_f.bias,
+               lm_head=model.lm_head.weight)
+    return spec, top, layers
+
+
+def _phi(model):
+    """Phi-1/1.5/2 (reference v2 `model_implementations/phi/`): GPT-J-like parallel block with one shared
+    LayerNorm, partial rotary (NeoX half-split over the first rotary_dim lanes), biased q/k/v/dense/fc1/fc2,
+    gelu_new, final LayerNorm and a biased LM head."""
+    cfg = model.config
+    H, nh = cfg.hidden_size, cfg.num_attention_heads
+    hd = H // nh
+    theta, partial = _rope(cfg)
+    assert not getattr(cfg, "qk_layernorm", False), "Phi qk_layernorm variant unsupported"
+    spec = DSModelSpec(arch="phi", vocab_size=cfg.vocab_size, hidden_size=H, num_layers=cfg.num_hidden_layers,
+                       num_heads=nh, num_kv_heads=getattr(cfg, "num_key_value_heads", None) or nh,
+                       intermediate_size=cfg.intermediate_size, norm="ln", norm_eps=cfg.layer_norm_eps, pos="rope",
+                       rope_theta=theta, rotary_dim=int(hd * partial), act=cfg.hidden_act, gated_mlp=False,
+                       qkv_bias=True, o_bias=True, mlp_bias=True, parallel_residual=True, shared_parallel_norm=True,
+                       max_positions=cfg.max_position_embeddings, lm_head_bias=True,
+                       tie_embeddings=bool(getattr(cfg, "tie_word_embeddings", False)))
+    base = model.model
+    layers = []
+    for L in base.layers:
+        a, mlp = L.self_attn, L.mlp
+        layers.append(dict(ln1_w=L.input_layernorm.weight, ln1_b=L.input_layernorm.bias, q_w=a.q_proj.weight,
+                           k_w=a.k_proj.weight, v_w=a.v_proj.weight, q_b=a.q_proj.bias, k_b=a.k_proj.bias,
+                           v_b=a.v_proj.bias, o_w=a.dense.weight, o_b=a.dense.bias, fc1_w=mlp.fc1.weight,
+                           fc1_b=mlp.fc1.bias, fc2_w=mlp.fc2.weight, fc2_b=mlp.fc2.bias))
+    top = dict(embed=base.embed_tokens.weight, norm_w=base.final_layernorm.weight,
+               norm_b=base.final_layernorm.bias, lm_head=model.lm_head.weight, lm_head_b=model.lm_head.bias)
+    return spec, top, layers
+
+
 CONVERTERS = {
     "llama": _llama_like, "mistral": _llama_like, "qwen2": _llama_like, "internlm": _llama_like,
     "gpt2": _gpt2, "bloom": _bloom, "opt": _opt, "gpt_neox": _gpt_neox, "gptj": _gptj,
+    "mixtral": _mixtral, "falcon": _falcon, "phi": _phi,
 }
 
 
@@ -267,7 +389,14 @@ def shard_layer(spec, lw, r, tp):
     out["o_w"] = _cols(lw["o_w"], r, tp)
     if lw.get("o_b") is not None:
         out["o_b"] = lw["o_b"]
-    if "gate_w" in lw:
+    if "experts_gate_up" in lw:  # [E, 2I, H] gate rows then up rows; [E, H, I]
+        gu = lw["experts_gate_up"]
+        I = gu.shape[1] // 2
+        n = I // tp
+        out["fc1_w"] = torch.cat([gu[:, r * n:(r + 1) * n], gu[:, I + r * n:I + (r + 1) * n]], 1)
+        out["fc2_w"] = lw["experts_down"][:, :, r * n:(r + 1) * n]
+        out["router_w"] = lw["router_w"]
+    elif "gate_w" in lw:
         out["fc1_w"] = torch.cat([_rows(lw["gate_w"], r, tp), _rows(lw["up_w"], r, tp)], 0)
         if lw.get("gate_b") is not None:
             out["fc1_b"] = torch.cat([_rows(lw["gate_b"], r, tp), _rows(lw["up_b"], r, tp)], 0)
@@ -275,7 +404,8 @@ def shard_layer(spec, lw, r, tp):
         out["fc1_w"] = _rows(lw["fc1_w"], r, tp)
         if lw.get("fc1_b") is not None:
             out["fc1_b"] = _rows(lw["fc1_b"], r, tp)
-    out["fc2_w"] = _cols(lw["fc2_w"], r, tp)
+    if "experts_down" not in lw:
+        out["fc2_w"] = _cols(lw["fc2_w"], r, tp)
     if lw.get("fc2_b") is not None:
         out["fc2_b"] = lw["fc2_b"]
     for n in ("ln1_w", "ln1_b", "ln2_w", "ln2_b"):

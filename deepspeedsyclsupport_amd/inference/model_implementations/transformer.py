@@ -53,6 +53,9 @@ class DSModelSpec:
     learned_pos_offset: int = 0      # OPT uses 2
     sliding_window: int = 0
     lm_head_bias: bool = False
+    num_experts: int = 0             # > 0: MoE MLP (Mixtral-style top-k router over gated experts)
+    moe_top_k: int = 2
+    moe_renormalize: bool = True     # renormalise the top-k routing weights to sum to 1
 
     def __post_init__(self):
         if not self.head_dim:
@@ -136,16 +139,23 @@ class DSInferenceLayer(nn.Module):
             if spec.qkv_bias else None
         self.o_w = nn.Parameter(torch.empty(H, self.hq * D, **kw), requires_grad=False)
         self.o_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.o_bias else None
-        self.fc1_w = nn.Parameter(torch.empty((2 if spec.gated_mlp else 1) * I, H, **kw), requires_grad=False)
-        self.fc1_b = nn.Parameter(torch.zeros((2 if spec.gated_mlp else 1) * I, **kw), requires_grad=False) \
-            if spec.mlp_bias else None
-        self.fc2_w = nn.Parameter(torch.empty(H, I, **kw), requires_grad=False)
-        self.fc2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.mlp_bias else None
+        G = 2 if spec.gated_mlp else 1
+        E = spec.num_experts
+        if E:  # experts stacked [E, ...] and sharded by intermediate (TP) like a dense MLP; router replicated
+            self.router_w = nn.Parameter(torch.empty(E, H, **kw), requires_grad=False)
+            self.fc1_w = nn.Parameter(torch.empty(E, G * I, H, **kw), requires_grad=False)
+            self.fc2_w = nn.Parameter(torch.empty(E, H, I, **kw), requires_grad=False)
+        else:
+            self.router_w = None
+            self.fc1_w = nn.Parameter(torch.empty(G * I, H, **kw), requires_grad=False)
+            self.fc2_w = nn.Parameter(torch.empty(H, I, **kw), requires_grad=False)
+        self.fc1_b = nn.Parameter(torch.zeros(G * I, **kw), requires_grad=False) if spec.mlp_bias and not E else None
+        self.fc2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.mlp_bias and not E else None
         self.quant = {}
 
     # ------------------------------------------------------------------------------------------ helpers
     def quantize_weights(self, bits=8, group_size=64):
-        for name in ("qkv_w", "o_w", "fc1_w", "fc2_w"):
+        for name in ("qkv_w", "o_w") + (() if self.spec.num_experts else ("fc1_w", "fc2_w")):
             self.quant[name] = QuantLinearWeight(getattr(self, name).data, bits, group_size)
             getattr(self, name).data = torch.empty(0, dtype=getattr(self, name).dtype,
                                                    device=getattr(self, name).device)
@@ -209,7 +219,43 @@ class DSInferenceLayer(nn.Module):
             out = out + self.o_b
         return out
 
+    def _act(self, h):
+        if self.spec.gated_mlp:
+            return DF.gated_activation(h, self.spec.act)
+        return DF.bias_activation(h, None, self.spec.act)
+
+    def _moe(self, x):
+        """Top-k routed experts (reference v2 `modules/implementations/moe/cutlass_multi_gemm.py` +
+        `kernels/ragged_ops/top_k_gating`): fp32 softmax router -> top-k -> tokens grouped by expert (one sort) ->
+        one GEMM pair per active expert -> weighted scatter-add. Experts are TP-sharded along the intermediate dim,
+        so one all-reduce finishes the block exactly like a dense MLP."""
+        shp = x.shape
+        t = x.reshape(-1, shp[-1])
+        probs = torch.softmax(F.linear(t, self.router_w).float(), dim=-1)
+        topw, topi = torch.topk(probs, self.spec.moe_top_k, dim=-1)
+        if self.spec.moe_renormalize:
+            topw = topw / topw.sum(-1, keepdim=True)
+        flat = topi.reshape(-1)
+        order = torch.argsort(flat, stable=True)
+        counts = torch.bincount(flat, minlength=self.spec.num_experts).tolist()
+        tok = order // self.spec.moe_top_k
+        wts = topw.reshape(-1)[order]
+        out = torch.zeros(t.shape, dtype=torch.float32, device=t.device)
+        s = 0
+        for e, c in enumerate(counts):
+            if c == 0:
+                continue
+            rows, w = tok[s:s + c], wts[s:s + c]
+            s += c
+            h = self._act(F.linear(t.index_select(0, rows), self.fc1_w[e]))
+            y = F.linear(h, self.fc2_w[e])
+            out.index_add_(0, rows, y.float() * w[:, None])
+        out = self._allreduce(out.to(x.dtype)).view(shp)
+        return out
+
     def _mlp(self, x):
+        if self.spec.num_experts:
+            return self._moe(x)
         h = F.linear(x, self._w("fc1_w"), self.fc1_b)
         if self.spec.gated_mlp:
             h = DF.gated_activation(h, self.spec.act)
@@ -225,7 +271,7 @@ class DSInferenceLayer(nn.Module):
     def _skinny_ok(self, h):
         spec = self.spec
         return (h.is_cuda and h.dtype == torch.bfloat16 and not self.quant and spec.norm == "rms"
-                and not spec.parallel_residual and _skinny_rows_ok(h.numel() // h.shape[-1], spec.hidden_size,
+                and not spec.parallel_residual and not spec.num_experts and _skinny_rows_ok(h.numel() // h.shape[-1], spec.hidden_size,
                                                                     spec.intermediate_size // self.tp,
                                                                     self.hq * spec.head_dim))
 

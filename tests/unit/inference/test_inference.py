@@ -47,10 +47,28 @@ def tiny(kind, H=64):
     if kind == "gptj":
         return T.GPTJForCausalLM(T.GPTJConfig(vocab_size=V, n_embd=H, n_layer=2, n_head=4, rotary_dim=8,
                                               n_positions=128, bos_token_id=0, eos_token_id=1))
+    if kind == "mixtral":
+        c = T.MixtralConfig(vocab_size=V, hidden_size=H, intermediate_size=2 * H, num_hidden_layers=2,
+                            num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128,
+                            num_local_experts=4, num_experts_per_tok=2)
+        return T.MixtralForCausalLM(c)
+    if kind in ("falcon", "falcon_new", "falcon_seq"):
+        kw = dict(vocab_size=V, hidden_size=H, num_hidden_layers=2, num_attention_heads=4,
+                  max_position_embeddings=128, bos_token_id=0, eos_token_id=1)
+        if kind == "falcon_new":  # 40B/180B layout: grouped kv heads, ln_attn + ln_mlp
+            kw.update(new_decoder_architecture=True, num_kv_heads=2)
+        if kind == "falcon_seq":  # sequential residual, full MHA with interleaved qkv, biased linears
+            kw.update(parallel_attn=False, multi_query=False, bias=True)
+        return T.FalconForCausalLM(T.FalconConfig(**kw))
+    if kind == "phi":
+        return T.PhiForCausalLM(T.PhiConfig(vocab_size=V, hidden_size=H, intermediate_size=2 * H,
+                                            num_hidden_layers=2, num_attention_heads=4, max_position_embeddings=128,
+                                            partial_rotary_factor=0.5, bos_token_id=0, eos_token_id=1))
     raise ValueError(kind)
 
 
-ARCHS = ["llama", "mistral", "qwen2", "gpt2", "bloom", "opt", "gpt_neox", "gptj"]
+ARCHS = ["llama", "mistral", "qwen2", "gpt2", "bloom", "opt", "gpt_neox", "gptj", "mixtral", "falcon", "falcon_new",
+         "falcon_seq", "phi"]
 
 
 def _ids(B=2, S=12, seed=1):
@@ -152,7 +170,7 @@ def _tp_run(kind, inject):
         assert torch.equal(eng.generate(ids, max_new_tokens=4), g_ref)
 
 
-@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt2"])
+@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt2", "mixtral", "falcon", "falcon_new", "phi"])
 def test_tp2_injected(kind):
     run_distributed(_tp_run, 2, kind, True)
 
@@ -164,7 +182,7 @@ def test_tp2_autotp(kind):
 
 # ---------------------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt_neox"])
+@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt_neox", "mixtral", "falcon", "phi"])
 def test_injected_bf16_gpu(kind):
     import deepspeedsyclsupport_amd as ds
     m = tiny(kind, H=256).eval()
