@@ -147,12 +147,14 @@ def main():
     log(f"[bench] engine ready in {time.time() - t0:.1f}s; mem {mem_gib():.1f} GiB")
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    # a distinct synthetic batch for every micro-step (no repeated data for the model to memorise)
+    n_micro = (args.warmup + args.steps) * args.gas
     batches = [torch.randint(0, cfg.vocab_size, (args.micro_batch, args.seq_len), device=dev, generator=g)
-               for _ in range(2)]
+               for _ in range(n_micro)]
 
     def train_step(i):
         for a in range(args.gas):
-            x = batches[(i + a) % 2]
+            x = batches[i * args.gas + a]
             loss = engine(x, labels=x)
             engine.backward(loss)
             engine.step()
@@ -168,7 +170,7 @@ def main():
     sync()
     t_start = time.perf_counter()
     for i in range(args.steps):
-        loss = train_step(i)
+        loss = train_step(args.warmup + i)
         if rank == 0 and (i + 1) % max(1, args.steps // 5) == 0:
             log(f"[bench] step {i + 1}/{args.steps}")
     sync()

@@ -39,6 +39,8 @@ int ds_qkv_rope_bwd(const void*, const void*, const void*, void*, const float*, 
                     int, int, int, int, int, int, hipStream_t);
 int ds_rope_inplace(void*, int, int, int, int, int64_t, int64_t, int64_t, const float*, const float*, const int*, int,
                     int, int, int, int, hipStream_t);
+int ds_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*,
+                 const int64_t*, const int64_t*, const int64_t*, float, int, hipStream_t);
 int ds_xent_fwd(const void*, const int64_t*, float*, float*, int64_t, int, int64_t, int, float, int, hipStream_t);
 int ds_xent_bwd(const void*, const int64_t*, const float*, const float*, float, void*, int64_t, int, int64_t, int64_t,
                 int, float, int, hipStream_t);
@@ -345,13 +347,44 @@ Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, OptT dloss, double dlo
   return out;
 }
 
+// ------------------------------------------------------------------------------------------ flash attention
+// q [B,Hq,S,128] / k,v [B,Hk,Skv,128] bf16 views with unit last stride; returns (o [B,Hq,S,128] whose memory is laid
+// out [B,S,Hq,128] so the o_proj GEMM reads it without a transpose copy, lse [B,Hq,S] fp32).
+std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale, bool want_lse) {
+  TORCH_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "flash_fwd: device tensors expected");
+  TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "flash_fwd: 4-D [B,H,S,D] tensors expected");
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 && v.scalar_type() == at::kBFloat16,
+              "flash_fwd: bf16 only");
+  TORCH_CHECK(q.size(3) == 128 && k.size(3) == 128 && v.size(3) == 128, "flash_fwd: head dim 128 only");
+  TORCH_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1, "flash_fwd: unit last stride required");
+  const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), Hk = k.size(1), Skv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Hk && v.size(2) == Skv, "flash_fwd: k/v shape");
+  TORCH_CHECK(Hq % Hk == 0, "flash_fwd: Hq must be a multiple of Hk");
+  for (const Tensor* t : {&q, &k, &v})
+    for (int d = 0; d < 3; ++d) TORCH_CHECK(t->stride(d) % 8 == 0, "flash_fwd: strides must be multiples of 8");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(q.data_ptr()) | reinterpret_cast<uintptr_t>(k.data_ptr()) |
+               reinterpret_cast<uintptr_t>(v.data_ptr())) % 16 == 0, "flash_fwd: 16-B aligned data required");
+  auto o = torch::empty({B, S, Hq, 128}, q.options()).transpose(1, 2);  // [B,Hq,S,D] view of [B,S,Hq,D] memory
+  Tensor lse;
+  if (want_lse) lse = torch::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  const int64_t qs[3] = {q.stride(0), q.stride(1), q.stride(2)}, ks[3] = {k.stride(0), k.stride(1), k.stride(2)},
+                vs[3] = {v.stride(0), v.stride(1), v.stride(2)}, os[3] = {o.stride(0), o.stride(1), o.stride(2)};
+  check(ds_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                     want_lse ? lse.data_ptr<float>() : nullptr, (int)B, (int)Hq, (int)Hk, (int)S, (int)Skv, qs, ks,
+                     vs, os, (float)scale, causal ? 1 : 0, stream()),
+        "flash_fwd");
+  return {o, lse};
+}
+
 }  // namespace
 
 // other binding translation units of this extension
 void register_inference_ops(pybind11::module& m);  // bind/infer_bind.cpp
+void register_host_mem_ops(pybind11::module& m);   // bind/host_mem.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_inference_ops(m);
+  register_host_mem_ops(m);
   m.doc() = "deepspeedsyclsupport_amd gfx950 kernels";
   m.def("adam_flat", &adam_flat);
   m.def("adam_multi", &adam_multi);
@@ -371,6 +404,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("qkv_rope_fwd", &qkv_rope_fwd);
   m.def("qkv_rope_bwd", &qkv_rope_bwd);
   m.def("rope_inplace", &rope_inplace);
+  m.def("flash_fwd", &flash_fwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
 }

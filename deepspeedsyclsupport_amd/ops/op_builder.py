@@ -39,11 +39,12 @@ EXTENSIONS = {
             "rope/rope_kernels.hip",
             "xent/xent_kernels.hip",
             "attn/decode_attn.hip",
+            "attn/flash_fwd.hip",
             "quant/quant_kernels.hip",
             "gemv/skinny_gemm.hip",
             "gemv/skinny_mfma.hip",
         ],
-        "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp"],
+        "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp", "bind/host_mem.cpp"],
     },
     # host ops: CPU Adam/Adagrad/Lion (ZeRO-Offload, Twin-Flow), async tensor I/O (ZeRO-Infinity), shm all-reduce
     "ds_cpu_ops": {
