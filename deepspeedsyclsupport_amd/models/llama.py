@@ -120,7 +120,7 @@ class LlamaAttention(nn.Module):
         B, S, _ = x.shape
         qkv = self.qkv_proj(x).view(B, S, self.nh + 2 * self.nkv, self.hd)
         q, k, v = DF.qkv_rope_split(qkv, rope.cos, rope.sin, self.nh, self.nkv, position_ids=position_ids,
-                                    pos_offset=pos_offset)
+                                    pos_offset=pos_offset, token_major=self.seq_parallel is None)
         if self.seq_parallel is not None:
             o = self.seq_parallel(q, k, v)  # [B, Hq, S, D] (local sequence shard)
         else:

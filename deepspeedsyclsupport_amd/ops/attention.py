@@ -40,6 +40,16 @@ def _sdpa(q, k, v, causal, scale, attn_mask=None, dropout_p=0.0):
     return F.scaled_dot_product_attention(q, k, v, **kw)
 
 
+_ZEROS = {}
+
+
+def _zero_seed(device):
+    z = _ZEROS.get(device)
+    if z is None:
+        z = _ZEROS[device] = torch.zeros((), dtype=torch.int64, device=device)
+    return z
+
+
 class FlashAttnFunc(torch.autograd.Function):
     """Forward: gfx950 flash kernel (O, LSE). Backward: efficient-attention backward on that (O, LSE)."""
 
@@ -60,10 +70,10 @@ class FlashAttnFunc(torch.autograd.Function):
         rep = hq // hk
         ke = k.repeat_interleave(rep, dim=1) if rep > 1 else k
         ve = v.repeat_interleave(rep, dim=1) if rep > 1 else v
-        z = torch.zeros((), dtype=torch.int64, device=q.device)
+        z = _zero_seed(q.device)  # no dropout: philox seed/offset unused
+        do = do if do.stride(-1) == 1 else do.contiguous()
         dq, dk, dv, _ = torch.ops.aten._scaled_dot_product_efficient_attention_backward(
-            do.contiguous(), q, ke, ve, None, o, lse, z, z, 0.0, [True, True, True, False], ctx.causal,
-            scale=ctx.scale)
+            do, q, ke, ve, None, o, lse, z, z, 0.0, [True, True, True, False], ctx.causal, scale=ctx.scale)
         if rep > 1:
             B, _, S, D = dk.shape
             dk = dk.view(B, hk, rep, S, D).sum(2)

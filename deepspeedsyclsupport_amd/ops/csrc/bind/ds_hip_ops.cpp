@@ -34,9 +34,9 @@ int ds_bias_act_fwd(const void*, const void*, void*, int64_t, int, int, int, hip
 int ds_bias_act_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 int ds_bias_residual(const void*, const void*, const void*, void*, int64_t, int, float, int, hipStream_t);
 int ds_qkv_rope_fwd(const void*, void*, void*, void*, const float*, const float*, const int*, int, int, int, int, int,
-                    int, int, int, hipStream_t);
+                    int, int, const int64_t*, int, hipStream_t);
 int ds_qkv_rope_bwd(const void*, const void*, const void*, void*, const float*, const float*, const int*, int, int,
-                    int, int, int, int, int, int, hipStream_t);
+                    int, int, int, int, int, const int64_t*, int, hipStream_t);
 int ds_rope_inplace(void*, int, int, int, int, int64_t, int64_t, int64_t, const float*, const float*, const int*, int,
                     int, int, int, int, hipStream_t);
 int ds_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*,
@@ -276,35 +276,55 @@ Tensor bias_residual(Tensor x, OptT bias, OptT res, double res_scale) {
 }
 
 // ------------------------------------------------------------------------------------------ rotary
+void hm_strides(const Tensor& q, const Tensor& k, const Tensor& v, int64_t (&st)[9]) {
+  const Tensor* ts[3] = {&q, &k, &v};
+  for (int i = 0; i < 3; ++i) {
+    TORCH_CHECK(ts[i]->dim() == 4 && ts[i]->stride(3) == 1, "q/k/v views need a unit last stride");
+    for (int d = 0; d < 3; ++d) st[3 * i + d] = ts[i]->stride(d);
+  }
+}
+
+// token_major: q/k/v are returned as [B,H,S,D] views of [B,S,H,D] memory (the layout the flash-attention kernel and
+// the efficient-attention backward exchange without transposing copies); else contiguous [B,H,S,D].
 std::vector<Tensor> qkv_rope_fwd(Tensor qkv, Tensor cos_t, Tensor sin_t, OptT pos, int64_t Hq, int64_t Hk, int64_t rot,
-                                 int64_t pos_offset) {
+                                 int64_t pos_offset, bool token_major) {
   need(qkv, "qkv"); need(cos_t, "cos"); need(sin_t, "sin");
   TORCH_CHECK(qkv.dim() == 4 && qkv.size(2) == Hq + 2 * Hk, "qkv must be [B,S,Hq+2Hk,D]");
   TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat, "cos/sin tables must be fp32");
   const int B = (int)qkv.size(0), S = (int)qkv.size(1), D = (int)qkv.size(3);
   TORCH_CHECK(cos_t.size(-1) == rot / 2, "cos table width must be rot/2");
   TORCH_CHECK(pos.has_value() || cos_t.size(0) >= S + pos_offset, "rotary table too short");
-  auto q = torch::empty({B, Hq, S, D}, qkv.options());
-  auto k = torch::empty({B, Hk, S, D}, qkv.options());
-  auto v = torch::empty({B, Hk, S, D}, qkv.options());
+  auto mk = [&](int64_t H) {
+    return token_major ? torch::empty({B, S, H, D}, qkv.options()).transpose(1, 2)
+                       : torch::empty({B, H, S, D}, qkv.options());
+  };
+  auto q = mk(Hq), k = mk(Hk), v = mk(Hk);
+  int64_t st[9];
+  hm_strides(q, k, v, st);
   const int* pp = nullptr;
   if (pos.has_value()) { need(*pos, "pos"); TORCH_CHECK(pos->scalar_type() == at::kInt, "pos int32"); pp = pos->data_ptr<int>(); }
   check(ds_qkv_rope_fwd(qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cos_t.data_ptr<float>(),
-                        sin_t.data_ptr<float>(), pp, B, S, (int)Hq, (int)Hk, D, (int)rot, (int)pos_offset, dcode(qkv),
-                        stream()),
+                        sin_t.data_ptr<float>(), pp, B, S, (int)Hq, (int)Hk, D, (int)rot, (int)pos_offset, st,
+                        dcode(qkv), stream()),
         "qkv_rope_fwd");
   return {q, k, v};
 }
 
+// dq/dk/dv: any [B,H,S,D] views with unit last stride (no contiguous copies)
 Tensor qkv_rope_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cos_t, Tensor sin_t, OptT pos, int64_t rot,
                     int64_t pos_offset) {
-  auto dqc = dq.contiguous(), dkc = dk.contiguous(), dvc = dv.contiguous();
+  TORCH_CHECK(dq.is_cuda() && dk.is_cuda() && dv.is_cuda(), "qkv_rope_bwd: device tensors");
+  Tensor dq_ = dq.stride(3) == 1 ? dq : dq.contiguous(), dk_ = dk.stride(3) == 1 ? dk : dk.contiguous(),
+         dv_ = dv.stride(3) == 1 ? dv : dv.contiguous();
   const int B = (int)dq.size(0), Hq = (int)dq.size(1), S = (int)dq.size(2), D = (int)dq.size(3);
   const int Hk = (int)dk.size(1);
   auto dqkv = torch::empty({B, S, Hq + 2 * Hk, D}, dq.options());
+  int64_t st[9];
+  hm_strides(dq_, dk_, dv_, st);
   const int* pp = pos.has_value() ? pos->data_ptr<int>() : nullptr;
-  check(ds_qkv_rope_bwd(dqc.data_ptr(), dkc.data_ptr(), dvc.data_ptr(), dqkv.data_ptr(), cos_t.data_ptr<float>(),
-                        sin_t.data_ptr<float>(), pp, B, S, Hq, Hk, D, (int)rot, (int)pos_offset, dcode(dq), stream()),
+  check(ds_qkv_rope_bwd(dq_.data_ptr(), dk_.data_ptr(), dv_.data_ptr(), dqkv.data_ptr(), cos_t.data_ptr<float>(),
+                        sin_t.data_ptr<float>(), pp, B, S, Hq, Hk, D, (int)rot, (int)pos_offset, st, dcode(dq),
+                        stream()),
         "qkv_rope_bwd");
   return dqkv;
 }
@@ -401,7 +421,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("bias_residual", &bias_residual);
-  m.def("qkv_rope_fwd", &qkv_rope_fwd);
+  m.def("qkv_rope_fwd", &qkv_rope_fwd, py::arg("qkv"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("hq"),
+        py::arg("hk"), py::arg("rot"), py::arg("pos_offset"), py::arg("token_major") = false);
   m.def("qkv_rope_bwd", &qkv_rope_bwd);
   m.def("rope_inplace", &rope_inplace);
   m.def("flash_fwd", &flash_fwd);

@@ -30,6 +30,12 @@ __device__ __forceinline__ void rot_pairs(float (&a)[8], float (&b)[8], const fl
   }
 }
 
+// element strides (batch, head, seq) of the head-major q / k / v views (unit last stride): [B,H,S,D] contiguous or a
+// [B,S,H,D]-memory view (token-major, what the flash kernel and the efficient backward exchange without copies)
+struct HmStrides {
+  int64_t q[3], k[3], v[3];
+};
+
 // Forward: qkv [B,S,NH,D] (NH = Hq + 2*Hk) -> q [B,Hq,S,D], k [B,Hk,S,D], v [B,Hk,S,D]; rope on q,k first `rot` dims.
 // Backward (INV): dq,dk,dv [B,H,S,D] -> dqkv [B,S,NH,D] with inverse rotation.
 // pos: optional int32 [B*S] position ids (else s + pos_offset).
@@ -40,7 +46,7 @@ __global__ void __launch_bounds__(256) qkv_rope_kernel(const T* __restrict__ qkv
                                                        T* __restrict__ k_out, T* __restrict__ v_out,
                                                        const float* __restrict__ cos_t, const float* __restrict__ sin_t,
                                                        const int* __restrict__ pos, int B, int S, int Hq, int Hk,
-                                                       int D, int rot, int pos_offset) {
+                                                       int D, int rot, int pos_offset, HmStrides st) {
   const int NH = Hq + 2 * Hk;
   const int half = rot / 2;
   // work item = (token, head, 16-element chunk): rotary chunks cover pairs, the rest plain 8-wide copies
@@ -60,12 +66,12 @@ __global__ void __launch_bounds__(256) qkv_rope_kernel(const T* __restrict__ qkv
     T* hm_dst;
     int hh;
     bool do_rot;
-    if (h < Hq) { hh = h; do_rot = true; hm_src = q_in; hm_dst = q_out; }
-    else if (h < Hq + Hk) { hh = h - Hq; do_rot = true; hm_src = k_in; hm_dst = k_out; }
-    else { hh = h - Hq - Hk; do_rot = false; hm_src = v_in; hm_dst = v_out; }
-    const int Hh = (h < Hq) ? Hq : Hk;
+    const int64_t* sd;
+    if (h < Hq) { hh = h; do_rot = true; hm_src = q_in; hm_dst = q_out; sd = st.q; }
+    else if (h < Hq + Hk) { hh = h - Hq; do_rot = true; hm_src = k_in; hm_dst = k_out; sd = st.k; }
+    else { hh = h - Hq - Hk; do_rot = false; hm_src = v_in; hm_dst = v_out; sd = st.v; }
     const int64_t tm_off = (tok * NH + h) * (int64_t)D;                       // token-major [B,S,NH,D]
-    const int64_t hm_off = (((int64_t)b * Hh + hh) * S + s) * (int64_t)D;   // head-major [B,H,S,D]
+    const int64_t hm_off = b * sd[0] + hh * sd[1] + s * sd[2];              // head-major view [B,H,S,D]
     const T* src = INV ? hm_src + hm_off : qkv_in + tm_off;
     T* dst = INV ? qkv_out + tm_off : hm_dst + hm_off;
     if (chunk < rot_chunks) {
@@ -127,26 +133,30 @@ __global__ void __launch_bounds__(256) rope_inplace_kernel(T* __restrict__ x, in
 
 extern "C" int ds_qkv_rope_fwd(const void* qkv, void* q, void* k, void* v, const float* cos_t, const float* sin_t,
                                const int* pos, int B, int S, int Hq, int Hk, int D, int rot, int pos_offset,
-                               int dtype, hipStream_t s) {
+                               const int64_t* strides9, int dtype, hipStream_t s) {
+  HmStrides st;
+  for (int i = 0; i < 3; ++i) { st.q[i] = strides9[i]; st.k[i] = strides9[3 + i]; st.v[i] = strides9[6 + i]; }
   if (D % 8 || rot % 16 || rot > D) return (int)hipErrorInvalidValue;
   const int64_t work = (int64_t)B * S * (Hq + 2 * Hk) * (rot / 16 + (D - rot) / 8);
   const int grid = ds_grid_for(work, 256);
   DISPATCH_T(dtype, hipLaunchKernelGGL((qkv_rope_kernel<T, false>), dim3(grid), dim3(256), 0, s, (const T*)qkv,
                                        nullptr, nullptr, nullptr, nullptr, (T*)q, (T*)k, (T*)v, cos_t, sin_t, pos, B,
-                                       S, Hq, Hk, D, rot, pos_offset));
+                                       S, Hq, Hk, D, rot, pos_offset, st));
   DS_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int ds_qkv_rope_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, const float* cos_t,
                                const float* sin_t, const int* pos, int B, int S, int Hq, int Hk, int D, int rot,
-                               int pos_offset, int dtype, hipStream_t s) {
+                               int pos_offset, const int64_t* strides9, int dtype, hipStream_t s) {
+  HmStrides st;
+  for (int i = 0; i < 3; ++i) { st.q[i] = strides9[i]; st.k[i] = strides9[3 + i]; st.v[i] = strides9[6 + i]; }
   if (D % 8 || rot % 16 || rot > D) return (int)hipErrorInvalidValue;
   const int64_t work = (int64_t)B * S * (Hq + 2 * Hk) * (rot / 16 + (D - rot) / 8);
   const int grid = ds_grid_for(work, 256);
   DISPATCH_T(dtype, hipLaunchKernelGGL((qkv_rope_kernel<T, true>), dim3(grid), dim3(256), 0, s, nullptr,
                                        (const T*)dq, (const T*)dk, (const T*)dv, (T*)dqkv, nullptr, nullptr, nullptr,
-                                       cos_t, sin_t, pos, B, S, Hq, Hk, D, rot, pos_offset));
+                                       cos_t, sin_t, pos, B, S, Hq, Hk, D, rot, pos_offset, st));
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -128,8 +128,8 @@ def bias_activation(x, bias, act="gelu"):
 class _QKVRopeFn(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, pos, hq, hk, rot, offset):
-        q, k, v = hip_ops().qkv_rope_fwd(qkv, cos, sin, pos, hq, hk, rot, offset)
+    def forward(ctx, qkv, cos, sin, pos, hq, hk, rot, offset, token_major=False):
+        q, k, v = hip_ops().qkv_rope_fwd(qkv, cos, sin, pos, hq, hk, rot, offset, token_major)
         ctx.save_for_backward(cos, sin, pos)
         ctx.rot, ctx.offset = rot, offset
         return q, k, v
@@ -138,18 +138,21 @@ class _QKVRopeFn(torch.autograd.Function):
     def backward(ctx, dq, dk, dv):
         cos, sin, pos = ctx.saved_tensors
         dqkv = hip_ops().qkv_rope_bwd(dq, dk, dv, cos, sin, pos, ctx.rot, ctx.offset)
-        return dqkv, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None
 
 
-def qkv_rope_split(qkv, cos, sin, num_heads, num_kv_heads, rotary_dim=None, position_ids=None, pos_offset=0):
+def qkv_rope_split(qkv, cos, sin, num_heads, num_kv_heads, rotary_dim=None, position_ids=None, pos_offset=0,
+                   token_major=False):
     """qkv [B, S, Hq+2Hk, D] -> q [B,Hq,S,D], k [B,Hk,S,D], v [B,Hk,S,D] with rotate_half RoPE on q and k.
+    `token_major=True` returns them as views of [B,S,H,D] memory (what the flash-attention path exchanges with its
+    backward without transposing copies).
 
     `cos`/`sin` are fp32 tables [max_pos, rot/2] (see `reference.rope_tables`)."""
     B, S, NH, D = qkv.shape
     rot = rotary_dim or D
     if qkv.is_cuda and D % 8 == 0 and rot % 16 == 0:
         pos = position_ids.to(torch.int32).contiguous() if position_ids is not None else None
-        return _QKVRopeFn.apply(qkv.contiguous(), cos, sin, pos, num_heads, num_kv_heads, rot, pos_offset)
+        return _QKVRopeFn.apply(qkv.contiguous(), cos, sin, pos, num_heads, num_kv_heads, rot, pos_offset, token_major)
     q, k, v = qkv.split([num_heads, num_kv_heads, num_kv_heads], dim=2)
     p = position_ids if position_ids is not None else torch.arange(pos_offset, pos_offset + S, device=qkv.device)
     q = reference.apply_rope_half(q, cos, sin, p)

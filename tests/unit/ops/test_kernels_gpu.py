@@ -183,15 +183,17 @@ def test_bias_act(dtype):
     torch.testing.assert_close(x.grad.float(), xf.grad, **TOL[dtype])
 
 
+@pytest.mark.parametrize("token_major", [False, True])
 @pytest.mark.parametrize("hq,hk", [(8, 8), (8, 2)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_qkv_rope_split(hq, hk, dtype):
+def test_qkv_rope_split(hq, hk, dtype, token_major):
     from deepspeedsyclsupport_amd.ops.transformer import functional as DF
     torch.manual_seed(6)
     B, S, D = 2, 33, 128
     cos, sin = R.rope_tables(128, D, device="cuda")
     qkv = torch.randn(B, S, hq + 2 * hk, D, device="cuda", dtype=dtype, requires_grad=True)
-    q, k, v = DF.qkv_rope_split(qkv, cos, sin, hq, hk)
+    q, k, v = DF.qkv_rope_split(qkv, cos, sin, hq, hk, token_major=token_major)
+    assert q.transpose(1, 2).is_contiguous() == token_major
     qf = qkv.detach().float().requires_grad_(True)
     qq, kk, vv = qf.split([hq, hk, hk], dim=2)
     pos = torch.arange(S, device="cuda")
