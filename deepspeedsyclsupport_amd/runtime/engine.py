@@ -519,9 +519,10 @@ class DeepSpeedEngine(nn.Module):
         return os.path.join(checkpoints_path, str(tag), f"{prefix}{dp_rank}_mp_rank_{mp_rank:02d}{CK.OPTIM_FILE_SUFFIX}")
 
     def module_state_dict(self, destination=None, prefix="", keep_vars=False, exclude_frozen_parameters=False):
-        """Full module state dict; under ZeRO-3 (dp>1) this gathers every group (16-bit weights)."""
+        """Full module state dict; under ZeRO-3 (dp>1 or offloaded params) this gathers every group (16-bit)."""
         from .zero.partition_parameters import GatheredParameters
-        if self.zero_optimization_partition_weights() and self.dp_world_size > 1:
+        if self.zero_optimization_partition_weights() and (self.dp_world_size > 1 or
+                                                           getattr(self.optimizer, "offload_param", False)):
             with GatheredParameters(list(self.module.parameters())):
                 sd = {k: v.detach().clone() for k, v in self.module.state_dict().items()}
             return sd

@@ -68,16 +68,27 @@ class ParamCoordinator:
 
     # ----------------------------------------------------------------------------------- core
     def _gather(self, g):
-        """Fill g.full: hpZ intra-node re-gather in backward, qwZ int8 gather, or the plain bf16 all-gather."""
+        """Fill g.full: hpZ intra-node re-gather in backward, qwZ int8 gather, or the plain bf16 all-gather.
+        Offloaded shards (ZeRO-Infinity) are first streamed host->device on this same stream."""
         hpz = self.hpz if (self.hpz is not None and g.dp_group is self.opt.dp_group) else None
         if self.in_backward and hpz is not None and hpz.can_use(g):
             hpz.gather_from_secondary(g)
             return
-        if self.qwz:
+        shard = g.shard
+        if shard.device != g.full.device:
+            if not g.partition:
+                g.full[:g.seg].copy_(shard, non_blocking=shard.is_pinned())
+                return
+            staged = torch.empty(g.seg, dtype=shard.dtype, device=g.full.device)
+            staged.copy_(shard, non_blocking=shard.is_pinned())
+            shard = staged
+        if not g.partition:
+            g.full.copy_(shard)
+        elif self.qwz:
             from .zeropp import quantized_all_gather
-            quantized_all_gather(g.full, g.shard, g.dp_group)
+            quantized_all_gather(g.full, shard, g.dp_group)
         else:
-            dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
+            dist.all_gather_into_tensor(g.full, shard, group=g.dp_group)
         if hpz is not None and not self.in_backward:
             hpz.keep_secondary(g)
 

@@ -151,12 +151,24 @@ class FlatZeroOptimizer:
         self.nvme_swapper = None
         if self.offload and str(getattr(self.zc.offload_optimizer.device, "value",
                                         self.zc.offload_optimizer.device)) == "nvme":
-            import os
             from ..swap_tensor import OptimizerStateSwapper
             path = self.zc.offload_optimizer.nvme_path or "/tmp/ds_nvme_swap"
             folder = os.path.join(path, f"zero_stage_{self.stage}", "optimizer", f"rank{dist.get_rank()}")
             self.nvme_swapper = OptimizerStateSwapper(ds_config.aio_config, folder,
                                                       pin=self.device.type == "cuda")
+        # ZeRO-Infinity parameter offload: non-persistent ZeRO-3 shards live in pinned host memory (cpu) or in
+        # per-group files on NVMe mapped into the address space (nvme); every fetch streams them H2D on the
+        # all-gather stream ahead of use (trace-driven prefetch), so HBM only holds the live working set.
+        self.offload_param = False
+        self.param_store = None
+        op = self.zc.offload_param if self.zc is not None else None
+        if self.stage == 3 and op is not None and _devname(op.device) in ("cpu", "nvme"):
+            self.offload_param = True
+            if _devname(op.device) == "nvme":
+                from ..swap_tensor import ParamNvmeStore
+                folder = os.path.join(op.nvme_path or "/tmp/ds_nvme_swap", "zero_stage_3", "params",
+                                      f"rank{dist.get_rank()}")
+                self.param_store = ParamNvmeStore(folder)
         # fp16 loss scaling
         fp16 = dtype == torch.float16
         self.loss_scaler = CreateLossScaler(dtype, getattr(ds_config, "loss_scale", 0) or 1.0,
@@ -171,13 +183,14 @@ class FlatZeroOptimizer:
         self._build_master()
         self._install_grad_hooks()
         self.coordinator = None
-        if self.stage == 3 and self.dp > 1:
+        if self.stage == 3 and (self.dp > 1 or self.offload_param):
             from .coordinator import ParamCoordinator
             self.coordinator = ParamCoordinator(self, prefetch_bucket_size=self.zc.prefetch_bucket_size,
                                                 max_live_parameters=self.zc.max_live_parameters)
         log_dist(f"FlatZeroOptimizer: stage={self.stage} dp={self.dp} groups={len(self.groups)} "
                  f"params={sum(g.numel for g in self.groups) / 1e6:.1f}M partition={self.partition} "
-                 f"offload={self.offload}(ratio={self.offload_ratio}) fused_adam={self._fused_adam}", ranks=[0])
+                 f"offload={self.offload}(ratio={self.offload_ratio}) offload_param={self.offload_param} "
+                 f"fused_adam={self._fused_adam}", ranks=[0])
 
     # ================================================================================ construction
     def _trainable_params_in_order(self):
@@ -208,7 +221,8 @@ class FlatZeroOptimizer:
         if self.stage == 3:
             # one group per module that directly owns trainable params (fetch granularity = module), plus ONE
             # persistent group for every small param (< param_persistence_threshold): never released.
-            thr = self.zc.param_persistence_threshold if self.dp > 1 else 0
+            thr = self.zc.param_persistence_threshold if (self.dp > 1 or self.offload_param) else 0
+            fetched = self.dp > 1 or self.offload_param  # groups gathered / streamed in per module
             owned = set()
             persistent = []
             for name, m in self.module.named_modules():
@@ -222,7 +236,7 @@ class FlatZeroOptimizer:
                 persistent.extend(small)
                 if big:
                     big.sort(key=lambda p: self.param_to_og[id(p)])
-                    groups.append(dict(params=big, persistent=self.dp == 1, module=m))
+                    groups.append(dict(params=big, persistent=not fetched, module=m))
             rest = [p for p in self.opt_params if id(p) not in owned]
             persistent.extend(rest)
             if persistent:
@@ -246,7 +260,8 @@ class FlatZeroOptimizer:
             og = self.param_to_og[id(d["params"][0])]
             pg = self.og_dp_group[og]
             gdp, grank = dist.get_world_size(pg), dist.get_rank(pg)
-            g = FlatGroup(i, d["params"], gdp, grank, self.stage >= 1 and gdp > 1, d["persistent"] or gdp == 1,
+            persistent = d["persistent"] or (gdp == 1 and not self.offload_param)
+            g = FlatGroup(i, d["params"], gdp, grank, self.stage >= 1 and gdp > 1, persistent,
                           self.device, self.dtype, d["module"], dp_group=pg)
             self.groups.append(g)
         self.param_group = {}
@@ -280,8 +295,9 @@ class FlatZeroOptimizer:
                 self._point_params(g)
                 g.status = ZeroParamStatus.AVAILABLE
             else:
-                g.shard = full[g.seg_lo:g.seg_lo + g.seg].clone()
-                del full
+                seg = full[g.seg_lo:g.seg_lo + g.seg]
+                g.shard = self._offload_shard(g, seg) if self.offload_param else seg.clone()
+                del full, seg
                 g.full = None
                 self._release_params(g)
             for i, p in enumerate(g.params):
@@ -290,6 +306,18 @@ class FlatZeroOptimizer:
                 p.ds_group = g
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
+
+    def _offload_shard(self, g, seg):
+        """Host (pinned) or NVMe-backed home of an offloaded ZeRO-3 shard, initialised from `seg`."""
+        if self.param_store is not None:
+            return self.param_store.create(g.idx, seg)
+        if self.device.type == "cuda":
+            from ...ops.native import hip_ops
+            host = hip_ops().alloc_pinned(g.seg, self.dtype)  # exact size (torch's pinned pool rounds to 2^k)
+        else:
+            host = torch.empty(g.seg, dtype=self.dtype)
+        host.copy_(seg)
+        return host
 
     def _point_params(self, g):
         for i, p in enumerate(g.params):
@@ -345,10 +373,8 @@ class FlatZeroOptimizer:
         for og in range(self.num_og):
             self.master.append(torch.zeros(dev_len[og], dtype=torch.float32, device=self.device))
             self.grad_acc.append(None)  # fp32 accumulator, allocated only when a path needs it
-            self.master_host.append(torch.zeros(host_len[og], dtype=torch.float32, pin_memory=pin)
-                                    if host_len[og] else None)
-            self.grad_acc_host.append(torch.zeros(host_len[og], dtype=torch.float32, pin_memory=pin)
-                                      if host_len[og] else None)
+            self.master_host.append(_host_zeros(host_len[og], torch.float32, pin) if host_len[og] else None)
+            self.grad_acc_host.append(_host_zeros(host_len[og], torch.float32, pin) if host_len[og] else None)
         for g in self.groups:
             for (s, e, og, moff, on_host) in g.runs:
                 dst = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
@@ -704,8 +730,14 @@ class FlatZeroOptimizer:
                     gs = [gr for _, _, gr, _ in lst]
                     lps = [lp for _, _, _, lp in lst]
                     if fp.is_cuda:
+                        # offloaded shards: the kernel writes a device copy, streamed back to the host home after
+                        back = [(i, lp) for i, lp in enumerate(lps) if not lp.is_cuda]
+                        for i, lp in back:
+                            lps[i] = torch.empty(lp.numel(), dtype=lp.dtype, device=fp.device)
                         native.hip_ops().adam_multi(ps, ms, vs, gs, lps, group["lr"], b1, b2, group["eps"],
                                                     group["weight_decay"], bc1, bc2, grad_scale * s, adamw)
+                        for i, lp in back:
+                            lp.copy_(lps[i], non_blocking=lp.is_pinned())
                     else:
                         from ...ops import reference
                         for p_, m_, v_, g_, lp_ in zip(ps, ms, vs, gs, lps):
@@ -743,7 +775,7 @@ class FlatZeroOptimizer:
             b1, b2 = group["betas"]
             lp = self._host_lp.get(og)
             if lp is None:
-                lp = torch.empty(hp.numel(), dtype=self.dtype, pin_memory=self.device.type == "cuda")
+                lp = _host_zeros(hp.numel(), self.dtype, self.device.type == "cuda")
                 self._host_lp[og] = lp
             adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
             bc = group.get("bias_correction", True)
@@ -1037,6 +1069,21 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
+
+
+def _host_zeros(n, dtype, pin):
+    """Zeroed host buffer; pinned ones are allocated at their exact size (torch's pinned pool rounds every request
+    up to a power of two, which would waste up to half of a Twin-Flow partition's host memory)."""
+    if pin:
+        from ...ops.native import hip_ops
+        t = hip_ops().alloc_pinned(int(n), dtype)
+        t.zero_()
+        return t
+    return torch.zeros(int(n), dtype=dtype)
+
+
+def _devname(d):
+    return str(getattr(d, "value", d))
 
 
 def _version():

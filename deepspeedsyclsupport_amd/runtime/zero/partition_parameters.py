@@ -193,7 +193,11 @@ class GatheredParameters:
                 if g.status != ZeroParamStatus.AVAILABLE:
                     opt = g._opt
                     full = torch.empty(g.padded, dtype=g.dtype, device=g.device)
-                    dist.all_gather_into_tensor(full, g.shard, group=g.dp_group)
+                    shard = g.shard if g.shard.device == full.device else g.shard.to(full.device)  # offload_param
+                    if g.partition:
+                        dist.all_gather_into_tensor(full, shard, group=g.dp_group)
+                    else:
+                        full.copy_(shard)
                     g.full = full
                     opt._point_params(g)
                     g.status = ZeroParamStatus.AVAILABLE

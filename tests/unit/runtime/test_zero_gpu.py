@@ -28,12 +28,13 @@ def _torch_ref(steps, lr):
     return out
 
 
-def _engine(stage, dtype, steps, lr):
+def _engine(stage, dtype, steps, lr, zero_extra=None):
     import deepspeedsyclsupport_amd as ds
     from ..simple_model import base_config
     torch.manual_seed(0)
     m = tiny_llama(hidden_size=128, intermediate_size=256, num_attention_heads=4)
     cfg = base_config(stage=stage, lr=lr, mb=2, clip=1.0, dtype=dtype)
+    cfg["zero_optimization"].update(zero_extra or {})
     eng, _, _, _ = ds.initialize(model=m, config=cfg)
     out = []
     for x in _data(steps, 5):
@@ -55,3 +56,17 @@ def test_engine_bf16_tracks_fp32():
     ref = _torch_ref(6, 3e-3)
     got = _engine(3, "bf16", 6, 3e-3)
     assert got == pytest.approx(ref, rel=3e-2, abs=3e-2), (got, ref)
+
+
+@pytest.mark.parametrize("opt_dev", [None, "cpu"])
+@pytest.mark.parametrize("pdev", ["cpu", "nvme"])
+def test_param_offload_gpu_matches_device(pdev, opt_dev, tmp_path):
+    """ZeRO-Infinity on the device path: pinned-host / NVMe-mapped shards streamed H2D on the all-gather stream,
+    device Adam writing back through a device temp (or native CPU Adam for the offloaded optimizer)."""
+    extra = {"stage3_param_persistence_threshold": 1000,
+             "offload_param": {"device": pdev, "nvme_path": str(tmp_path)}}
+    if opt_dev:
+        extra["offload_optimizer"] = {"device": opt_dev}
+    ref = _engine(3, "fp32", 4, 3e-3)
+    got = _engine(3, "fp32", 4, 3e-3, extra)
+    assert got == pytest.approx(ref, rel=1e-4, abs=1e-4), (got, ref)
