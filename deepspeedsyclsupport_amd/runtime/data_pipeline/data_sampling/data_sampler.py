@@ -10,6 +10,26 @@ import numpy as np
 from ..curriculum_scheduler import CurriculumScheduler
 
 
+def _values_from_index(index_to_sample_path, index_to_metric_path, total):
+    """Per-sample difficulty from the analyzer's value-grouped index (group ordinal if no metric file is given)."""
+    from .indexed_dataset import MMapIndexedDataset
+    i2s = MMapIndexedDataset(index_to_sample_path)
+    i2m = MMapIndexedDataset(index_to_metric_path) if index_to_metric_path else None
+    vals = np.zeros(total, dtype=np.int64)
+    for row in range(len(i2s)):
+        vals[np.asarray(i2s[row], dtype=np.int64)] = int(i2m[row][0]) if i2m is not None else row
+    return vals
+
+
+def _load_sample_to_metric(path):
+    """A .npy array (loaded without pickle) or an MMIDIDX `<prefix>_sample_to_metric` dataset."""
+    if path.endswith(".npy"):
+        return np.load(path, mmap_mode="r")
+    from .indexed_dataset import MMapIndexedDataset
+    ds = MMapIndexedDataset(path)
+    return np.concatenate(ds[0:len(ds)]).astype(np.int64)
+
+
 class DeepSpeedDataSampler:
 
     def __init__(self, data_efficiency_config, one_epoch_total_samples, micro_batch_size, data_parallel_rank,
@@ -28,8 +48,11 @@ class DeepSpeedDataSampler:
         for name, mc in cl.get("curriculum_metrics", {}).items():
             self.schedulers[name] = CurriculumScheduler(mc)
             vals = metric_values.get(name) if metric_values else None
+            if vals is None and mc.get("index_to_sample_path"):
+                # DataAnalyzer output (reference config keys index_to_sample_path / index_to_metric_path)
+                vals = _values_from_index(mc["index_to_sample_path"], mc.get("index_to_metric_path"), self.total)
             if vals is None and mc.get("sample_to_metric_path"):
-                vals = np.load(mc["sample_to_metric_path"], mmap_mode="r")  # numpy, allow_pickle=False
+                vals = _load_sample_to_metric(mc["sample_to_metric_path"])
             self.metrics[name] = (np.asarray(vals), mc.get("difficulty_type", "value"))
         self.consumed_samples = 0
         self.curriculum_step = 0
