@@ -30,6 +30,9 @@ def parse_args(args=None):
     p.add_argument("--enable_elastic_training", action="store_true")
     p.add_argument("--min_elastic_nodes", type=int, default=-1)
     p.add_argument("--max_elastic_nodes", type=int, default=-1)
+    p.add_argument("--max_restarts", type=int, default=3, help="elastic: worker-group restarts before giving up")
+    p.add_argument("--heartbeat_timeout", type=float, default=0.0,
+                   help="elastic: restart the group when a rank's step heartbeat is older than this (s)")
     p.add_argument("--no_local_rank", action="store_true")
     p.add_argument("--save_pid", type=int, default=0, nargs="?", const=1)
     p.add_argument("--enable_each_rank_log", default="None", type=str)
@@ -108,6 +111,8 @@ def main(args=None):
     numactl = shutil.which("numactl")
     cores = parse_core_list(args.bind_core_list) if args.bind_core_list else None
     ranges = _core_ranges(len(envs), cores)
+    if args.enable_elastic_training:
+        return _run_elastic(args, envs)
     procs, logs = [], []
     for local_rank, renv in enumerate(envs):
         env = os.environ.copy()
@@ -167,6 +172,27 @@ def main(args=None):
     for f in logs:
         f.close()
     return rc
+
+
+def _run_elastic(args, envs):
+    """Supervise this node's ranks with the elastic agent (restart the group on failure, `--max_restarts`)."""
+    import tempfile
+    from ..elasticity.elastic_agent import DSElasticAgent, WorkerSpec
+    cmd = [] if args.no_python else [sys.executable, "-u"] + (["-m"] if args.module else [])
+    cmd += [args.training_script] + args.training_script_args
+    e0 = envs[0]
+    world, nproc = int(e0["WORLD_SIZE"]), len(envs)
+    common = {k: v for k, v in e0.items() if k not in ("RANK", "LOCAL_RANK")}
+    hb = tempfile.mkdtemp(prefix="ds_hb_") if args.heartbeat_timeout > 0 else None
+    spec = WorkerSpec(cmd=cmd, nproc=nproc, env=common, node_rank=int(e0.get("CROSS_RANK", 0)),
+                      nnodes=int(e0.get("CROSS_SIZE", 1)), rank_offset=int(e0["RANK"]), world_size=world,
+                      master_addr=e0["MASTER_ADDR"],
+                      master_port=int(e0["MASTER_PORT"]), max_restarts=args.max_restarts,
+                      log_dir=None if args.enable_each_rank_log == "None" else args.enable_each_rank_log,
+                      heartbeat_dir=hb, heartbeat_timeout=args.heartbeat_timeout)
+    res = DSElasticAgent(spec).run()
+    logger.info(f"elastic run {res.state} after {res.restarts} restart(s)")
+    return 0 if res.state == "SUCCEEDED" else 1
 
 
 if __name__ == "__main__":

@@ -186,6 +186,9 @@ class DeepSpeedEngine(nn.Module):
             self.device = torch.device("cpu")
         self.world_size = dist.get_world_size()
         self.global_rank = dist.get_rank()
+        from ..utils.fault_injection import FaultInjector
+        fi = FaultInjector(self.global_rank)
+        self._fault_injector = fi if fi.active else None
 
     def _configure_groups(self):
         sp = self._config.sequence_parallel_size
@@ -499,6 +502,8 @@ class DeepSpeedEngine(nn.Module):
                 self.monitor.write_events(ev)
             if self.global_steps % self.steps_per_print() == 0 and self.global_rank == 0:
                 log_dist(f"step={self.global_steps}, skipped={self.skipped_steps}, lr={self.get_lr()}", ranks=[0])
+            if self._fault_injector is not None:
+                self._fault_injector.on_step(self.global_steps)
         self.micro_steps += 1
         self.timers(STEP_MICRO_TIMER).stop()
 
