@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from ... import comm as dist
 from ...ops import reference
+from ...ops import moe_ops
 from ...ops.transformer import functional as DF
 
 
@@ -226,32 +227,12 @@ class DSInferenceLayer(nn.Module):
 
     def _moe(self, x):
         """Top-k routed experts (reference v2 `modules/implementations/moe/cutlass_multi_gemm.py` +
-        `kernels/ragged_ops/top_k_gating`): fp32 softmax router -> top-k -> tokens grouped by expert (one sort) ->
-        one GEMM pair per active expert -> weighted scatter-add. Experts are TP-sharded along the intermediate dim,
-        so one all-reduce finishes the block exactly like a dense MLP."""
-        shp = x.shape
-        t = x.reshape(-1, shp[-1])
-        probs = torch.softmax(F.linear(t, self.router_w).float(), dim=-1)
-        topw, topi = torch.topk(probs, self.spec.moe_top_k, dim=-1)
-        if self.spec.moe_renormalize:
-            topw = topw / topw.sum(-1, keepdim=True)
-        flat = topi.reshape(-1)
-        order = torch.argsort(flat, stable=True)
-        counts = torch.bincount(flat, minlength=self.spec.num_experts).tolist()
-        tok = order // self.spec.moe_top_k
-        wts = topw.reshape(-1)[order]
-        out = torch.zeros(t.shape, dtype=torch.float32, device=t.device)
-        s = 0
-        for e, c in enumerate(counts):
-            if c == 0:
-                continue
-            rows, w = tok[s:s + c], wts[s:s + c]
-            s += c
-            h = self._act(F.linear(t.index_select(0, rows), self.fc1_w[e]))
-            y = F.linear(h, self.fc2_w[e])
-            out.index_add_(0, rows, y.float() * w[:, None])
-        out = self._allreduce(out.to(x.dtype)).view(shp)
-        return out
+        `kernels/ragged_ops/top_k_gating`): fp32 softmax router -> top-k -> expert-contiguous scatter -> grouped
+        MFMA GEMM pair -> weighted gather, all on device without a host sync (`ops/moe_ops.py`). Experts are
+        TP-sharded along the intermediate dim, so one all-reduce finishes the block exactly like a dense MLP."""
+        out = moe_ops.moe_block(x, self.router_w, self.fc1_w, self.fc2_w, self.spec.moe_top_k, self._act,
+                                self.spec.moe_renormalize)
+        return self._allreduce(out)
 
     def _mlp(self, x):
         if self.spec.num_experts:
@@ -464,10 +445,12 @@ class DSInferenceModel(nn.Module):
 
     # ------------------------------------------------------------------------------------------ forward
     def _embed(self, input_ids, meta):
-        h = F.embedding(input_ids, self.embed)
         if self.pos_embed is not None:
+            # token + learned position rows in one gather kernel (reference `ragged_ops/embed/embed.cu:19`)
             pos = meta.pos_ids.view(input_ids.shape).long() + self.spec.learned_pos_offset
-            h = h + F.embedding(pos, self.pos_embed)
+            h = moe_ops.embed_gather(self.embed, input_ids, self.pos_embed, pos).view(*input_ids.shape, -1)
+        else:
+            h = F.embedding(input_ids, self.embed)
         if self.spec.embed_norm:
             h = DF.layer_norm(h, self.embed_ln_w, self.embed_ln_b, self.spec.norm_eps)
         return h

@@ -43,8 +43,9 @@ EXTENSIONS = {
             "quant/quant_kernels.hip",
             "gemv/skinny_gemm.hip",
             "gemv/skinny_mfma.hip",
+            "moe/moe_kernels.hip",
         ],
-        "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp", "bind/host_mem.cpp"],
+        "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp", "bind/moe_bind.cpp", "bind/host_mem.cpp"],
     },
     # host ops: CPU Adam/Adagrad/Lion (ZeRO-Offload, Twin-Flow), async tensor I/O (ZeRO-Infinity), shm all-reduce
     "ds_cpu_ops": {

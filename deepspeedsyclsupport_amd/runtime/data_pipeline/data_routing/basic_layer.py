@@ -4,10 +4,54 @@
 During training each wrapped layer processes only a random subset of `current_seq` tokens per sample (kept in
 their original order), the rest bypass it unchanged; at eval every token goes through. Gather / scatter along the
 sequence dimension are device index ops (one kernel each), the sorted random subset comes from a single
-`topk` over random keys per sample.
+`topk` over random keys per sample. For contiguous batch-first bf16 device activations they are the gfx950
+16-B-vector row gather / scatter kernels (`ops/moe_ops.py` rows_gather / rows_scatter) with their exact adjoints.
 """
 import torch
 import torch.nn as nn
+
+from ....ops import moe_ops
+
+
+def _native(x):
+    return x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[-1] % 8 == 0
+
+
+def _flat(idx, S):
+    return (idx + S * torch.arange(idx.shape[0], device=idx.device).unsqueeze(1)).reshape(-1)
+
+
+class _TokenGatherFn(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, flat):
+        ctx.save_for_backward(flat)
+        ctx.shape = x.shape
+        return moe_ops.rows_gather(x, flat)
+
+    @staticmethod
+    def backward(ctx, g):
+        (flat, ) = ctx.saved_tensors
+        dx = torch.zeros(ctx.shape, dtype=g.dtype, device=g.device)
+        moe_ops.rows_scatter(g.contiguous(), flat, dx)  # kept positions are distinct: scatter == scatter-add
+        return dx, None
+
+
+class _TokenScatterFn(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, full, part, flat):
+        ctx.save_for_backward(flat)
+        ctx.part_shape = part.shape
+        return moe_ops.rows_scatter(part.contiguous(), flat, full.clone())
+
+    @staticmethod
+    def backward(ctx, g):
+        (flat, ) = ctx.saved_tensors
+        g = g.contiguous()
+        gpart = moe_ops.rows_gather(g, flat).view(ctx.part_shape)
+        gfull = moe_ops.rows_scatter(torch.zeros_like(gpart), flat, g.clone())
+        return gfull, gpart, None
 
 
 def token_sort_(indices):
@@ -57,11 +101,19 @@ class RandomLayerTokenDrop(nn.Module):
         B = hidden_states.shape[0 if self.batch_first else 1]
         keys = torch.rand(B, S, device=hidden_states.device)
         idx = token_sort_(torch.topk(keys, self.reserved_length, dim=-1).indices)
-        part = token_gather(hidden_states, idx, self.batch_first)
+        native = self.batch_first and _native(hidden_states)
+        if native:
+            flat = _flat(idx, S)
+            part = _TokenGatherFn.apply(hidden_states, flat).view(B, self.reserved_length, -1)
+        else:
+            part = token_gather(hidden_states, idx, self.batch_first)
         out = self.random_ltd_layer(part, *args, **kwargs)
         rest = out[1:] if isinstance(out, tuple) else None
         out = out[0] if isinstance(out, tuple) else out
-        full = token_scatter_(hidden_states.clone(), out, idx, self.batch_first)
+        if native and out.dtype == hidden_states.dtype:
+            full = _TokenScatterFn.apply(hidden_states, out, flat)
+        else:
+            full = token_scatter_(hidden_states.clone(), out, idx, self.batch_first)
         return (full, ) + tuple(rest) if rest is not None else full
 
 
