@@ -33,6 +33,9 @@ int ds_gated_act_bwd(const void*, const void*, void*, int64_t, int, int, int, hi
 int ds_bias_act_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 int ds_bias_act_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 int ds_bias_residual(const void*, const void*, const void*, void*, int64_t, int, float, int, hipStream_t);
+int ds_dropout_fwd(const void*, const void*, const void*, void*, uint8_t*, int64_t, int, float, uint64_t, uint64_t, int,
+                   hipStream_t);
+int ds_dropout_bwd(const void*, void*, int64_t, int, float, uint64_t, uint64_t, int, hipStream_t);
 int ds_qkv_rope_fwd(const void*, void*, void*, void*, const float*, const float*, const int*, int, int, int, int, int,
                     int, int, const int64_t*, int, hipStream_t);
 int ds_qkv_rope_bwd(const void*, const void*, const void*, void*, const float*, const float*, const int*, int, int,
@@ -275,6 +278,35 @@ Tensor bias_residual(Tensor x, OptT bias, OptT res, double res_scale) {
   return y;
 }
 
+// ------------------------------------------------------------------------------------------ dropout
+// y = res + dropout_p(x + bias); the keep mask is a pure function of (seed, offset, element) so the backward
+// regenerates it. want_mask returns the packed mask (bit j of byte t = element 8t + j) for tests.
+std::vector<Tensor> dropout_fwd(Tensor x, OptT bias, OptT res, double p, int64_t seed, int64_t offset, bool want_mask) {
+  need(x, "x");
+  const int C = (int)x.size(-1);
+  TORCH_CHECK(C % 8 == 0, "dropout: last dim must be a multiple of 8");
+  if (bias.has_value()) TORCH_CHECK(bias->numel() == C && bias->scalar_type() == x.scalar_type(), "bias [C]");
+  if (res.has_value()) TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(), "residual shape");
+  auto y = torch::empty_like(x);
+  Tensor mask = want_mask ? torch::empty({x.numel() / 8}, x.options().dtype(at::kByte)) : Tensor();
+  check(ds_dropout_fwd(x.data_ptr(), ptr_or_null(bias), ptr_or_null(res), y.data_ptr(),
+                       want_mask ? mask.data_ptr<uint8_t>() : nullptr, x.numel() / C, C, (float)p, (uint64_t)seed,
+                       (uint64_t)offset, dcode(x), stream()),
+        "dropout_fwd");
+  if (want_mask) return {y, mask};
+  return {y};
+}
+
+Tensor dropout_bwd(Tensor dy, double p, int64_t seed, int64_t offset) {
+  need(dy, "dy");
+  const int C = (int)dy.size(-1);
+  auto dx = torch::empty_like(dy);
+  check(ds_dropout_bwd(dy.data_ptr(), dx.data_ptr(), dy.numel() / C, C, (float)p, (uint64_t)seed, (uint64_t)offset,
+                       dcode(dy), stream()),
+        "dropout_bwd");
+  return dx;
+}
+
 // ------------------------------------------------------------------------------------------ rotary
 void hm_strides(const Tensor& q, const Tensor& k, const Tensor& v, int64_t (&st)[9]) {
   const Tensor* ts[3] = {&q, &k, &v};
@@ -423,6 +455,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("bias_residual", &bias_residual);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("dropout_bwd", &dropout_bwd);
   m.def("qkv_rope_fwd", &qkv_rope_fwd, py::arg("qkv"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("hq"),
         py::arg("hk"), py::arg("rot"), py::arg("pos_offset"), py::arg("token_major") = false);
   m.def("qkv_rope_bwd", &qkv_rope_bwd);

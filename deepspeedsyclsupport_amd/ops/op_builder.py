@@ -36,6 +36,7 @@ EXTENSIONS = {
             "optim/optim_kernels.hip",
             "norm/norm_kernels.hip",
             "act/act_kernels.hip",
+            "act/dropout_kernels.hip",
             "rope/rope_kernels.hip",
             "xent/xent_kernels.hip",
             "attn/decode_attn.hip",

@@ -5,6 +5,7 @@ fused pieces of the reference training layer (`csrc/transformer/ds_transformer_c
 transform_0213, softmax) and inference kernels (`rms_norm.cu`, `apply_rotary_pos_emb.cu`, `gelu.cu` gated acts).
 """
 import torch
+import torch.nn.functional as F
 
 from .. import reference
 from ..native import hip_ops
@@ -122,6 +123,42 @@ def bias_activation(x, bias, act="gelu"):
     if x.is_cuda and x.shape[-1] % 8 == 0:
         return _BiasActFn.apply(x.contiguous(), bias, code)
     return reference.ACTS[code](x + bias if bias is not None else x)
+
+
+# --------------------------------------------------------------------------------------------------- dropout
+class _DropoutFn(torch.autograd.Function):
+    """y = residual + dropout_p(x + bias) in one kernel; the mask is regenerated from (seed, offset) in backward."""
+
+    @staticmethod
+    def forward(ctx, x, bias, residual, p, seed):
+        (y, ) = hip_ops().dropout_fwd(x, bias, residual, p, seed, 0, False)
+        ctx.p, ctx.seed, ctx.has_bias, ctx.has_res = p, seed, bias is not None, residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = hip_ops().dropout_bwd(dy, ctx.p, ctx.seed, 0)
+        db = dx.reshape(-1, dx.shape[-1]).sum(0) if ctx.has_bias else None
+        return dx, db, (dy if ctx.has_res else None), None, None
+
+
+def _dropout_seed():
+    # drawn from the host generator: reproducible under torch.manual_seed and restored by activation
+    # checkpointing's RNG stash, so a recomputed forward reproduces the same mask; no device sync
+    return int(torch.randint(0, 2**62, (1, )).item())
+
+
+def dropout(x, p, training=True, bias=None, residual=None):
+    """residual + dropout(x + bias) (reference `csrc/transformer/dropout_kernels.cu` fused variants)."""
+    if not training or p == 0.0:
+        y = x if bias is None else x + bias
+        return y if residual is None else y + residual
+    if x.is_cuda and x.shape[-1] % 8 == 0:
+        return _DropoutFn.apply(x.contiguous(), bias, None if residual is None else residual.contiguous(), float(p),
+                                _dropout_seed())
+    y = F.dropout(x if bias is None else x + bias, p, True)
+    return y if residual is None else y + residual
 
 
 # --------------------------------------------------------------------------------------------------- rotary + split

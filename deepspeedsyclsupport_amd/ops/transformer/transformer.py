@@ -140,7 +140,7 @@ class DeepSpeedTransformerLayer(nn.Module):
                 mask = mask[:, None, None, :]
         ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
         ctx = ctx.transpose(1, 2).reshape(B, S, H)
-        return F.linear(ctx, self.attn_ow, self.attn_ob)
+        return F.linear(ctx, self.attn_ow)  # output bias is fused into the dropout kernel
 
     def _ff(self, x):
         h = F.linear(x, self.inter_w)
@@ -148,7 +148,7 @@ class DeepSpeedTransformerLayer(nn.Module):
             h = checkpoint(lambda t: DF.bias_activation(t, self.inter_b, "gelu"), h, use_reentrant=False)
         else:
             h = DF.bias_activation(h, self.inter_b, "gelu")
-        return F.linear(h, self.output_w, self.output_b)
+        return F.linear(h, self.output_w)  # output bias is fused into the dropout kernel
 
     def forward(self, hidden_states, attention_mask=None, head_mask=None, layer_head_mask=None,
                 encoder_hidden_states=None, encoder_attention_mask=None, past_key_value=None,
@@ -158,13 +158,14 @@ class DeepSpeedTransformerLayer(nn.Module):
         pd = self.config.hidden_dropout_ratio if self.training else 0.0
         x = hidden_states
         if self.config.pre_layer_norm:
-            a = F.dropout(self._attention(self._ln(x, self.attn_nw, self.attn_nb), attention_mask), pd, self.training)
+            a = DF.dropout(self._attention(self._ln(x, self.attn_nw, self.attn_nb), attention_mask), pd,
+                           self.training, bias=self.attn_ob)
             normed, r = self._ln(a, self.norm_w, self.norm_b, residual=x)   # fused residual add + LN
-            out = r + F.dropout(self._ff(normed), pd, self.training)
+            out = DF.dropout(self._ff(normed), pd, self.training, bias=self.output_b, residual=r)
         else:
-            a = F.dropout(self._attention(x, attention_mask), pd, self.training)
+            a = DF.dropout(self._attention(x, attention_mask), pd, self.training, bias=self.attn_ob)
             r, _ = self._ln(a, self.attn_nw, self.attn_nb, residual=x)
-            f = F.dropout(self._ff(r), pd, self.training)
+            f = DF.dropout(self._ff(r), pd, self.training, bias=self.output_b)
             out, _ = self._ln(f, self.norm_w, self.norm_b, residual=r)
         if self.config.return_tuple:
             return (out, )

@@ -443,3 +443,57 @@ def test_qkv_rope_append(rot, interleaved):
             kr[blk, :, t % BS] = k.view(B, n, hk, D)[b, j]
             vr[blk, :, t % BS] = v.view(B, n, hk, D)[b, j]
     assert torch.equal(kc, kr) and torch.equal(vc, vr)
+
+
+def _unpack_mask(packed, shape):
+    bits = (packed.long().unsqueeze(-1) >> torch.arange(8, device=packed.device)) & 1
+    return bits.reshape(shape).bool()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_fused_dropout(dt, p):
+    """residual + dropout(x + bias) vs the same math in fp32 with the kernel's own mask; the mask's keep rate; the
+    backward regenerates the identical mask from the seed (no stored mask)."""
+    torch.manual_seed(0)
+    rows, C = 1000, 1024
+    x = torch.randn(rows, C, device="cuda").to(dt)
+    b = torch.randn(C, device="cuda").to(dt)
+    r = torch.randn(rows, C, device="cuda").to(dt)
+    y, packed = ops().dropout_fwd(x, b, r, p, 1234, 0, True)
+    keep = _unpack_mask(packed, (rows, C))
+    rate = keep.float().mean().item()
+    assert abs(rate - (1 - p)) < 0.01, rate
+    ref = r.float() + torch.where(keep, (x.float() + b.float()) / (1 - p), torch.zeros_like(x.float()))
+    torch.testing.assert_close(y.float(), ref, **TOL[dt])
+    dy = torch.randn(rows, C, device="cuda").to(dt)
+    dx = ops().dropout_bwd(dy, p, 1234, 0)
+    ref_dx = torch.where(keep, dy.float() / (1 - p), torch.zeros_like(dy.float()))
+    torch.testing.assert_close(dx.float(), ref_dx, **TOL[dt])
+    # a different seed gives a different mask; same seed the same one
+    _, p2 = ops().dropout_fwd(x, None, None, p, 1235, 0, True)
+    _, p3 = ops().dropout_fwd(x, None, None, p, 1234, 0, True)
+    assert not torch.equal(p2, packed) and torch.equal(p3, packed)
+
+
+def test_dropout_autograd_and_checkpoint_replay():
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(1)
+    # positive x and b: x + b is never 0, so y0 != 0 identifies the kept elements
+    x = (torch.rand(64, 256, device="cuda") + 0.1).bfloat16().requires_grad_(True)
+    b = (torch.rand(256, device="cuda") + 0.1).bfloat16().requires_grad_(True)
+    r = torch.randn(64, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    torch.manual_seed(7)
+    y0 = DF.dropout(x, 0.2, True, bias=b)
+    keep = y0 != 0
+    torch.manual_seed(7)
+    y = DF.dropout(x, 0.2, True, bias=b, residual=r)
+    torch.testing.assert_close(y.float(), (r.float() + y0.float()), rtol=2e-2, atol=2e-2)
+    y.float().sum().backward()
+    torch.testing.assert_close(x.grad.float(), keep.float() / 0.8, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(b.grad.float(), (keep.float() / 0.8).sum(0), rtol=2e-2, atol=2e-1)
+    assert torch.equal(r.grad, torch.ones_like(r))
+    torch.manual_seed(7)
+    y2 = torch.utils.checkpoint.checkpoint(lambda t: DF.dropout(t, 0.2, True, bias=b, residual=r), x,
+                                           use_reentrant=False)
+    assert torch.equal(y, y2)
