@@ -66,7 +66,14 @@ class InferenceEngine(torch.nn.Module):
             raise ValueError("init_inference expects an nn.Module (meta-tensor checkpoint loading: pass the model)")
 
         self.injected = False
-        if (config.replace_with_kernel_inject or _is_native(model)) and convert.supported(model):
+        self.encoder_injected = 0
+        from ..module_inject import encoder as enc
+        if config.replace_with_kernel_inject and not convert.supported(model) and enc.supported(model):
+            # bidirectional encoders (BERT family): fused layers swapped in place, HF embeddings / heads kept
+            dt = self.dtype if self.dtype in (torch.float16, torch.bfloat16, torch.float32) else torch.bfloat16
+            self.encoder_injected = enc.inject(model, self.mp_group, self.tp_size, self.tp_rank, dt, self.device)
+            self.module = model
+        elif (config.replace_with_kernel_inject or _is_native(model)) and convert.supported(model):
             self.module = convert.from_model(model, self.mp_group, self.tp_size, self.tp_rank, self.dtype, self.device,
                                              max_positions=config.max_out_tokens)
             self.injected = True

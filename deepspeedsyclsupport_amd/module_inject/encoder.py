@@ -1,0 +1,142 @@
+"""Kernel injection for bidirectional encoders: BERT / RoBERTa / XLM-R / ELECTRA / CamemBERT layers and DistilBERT
+blocks (reference `module_inject/containers/bert.py`, `containers/distil_bert.py`, the policy-driven
+`replace_transformer_layer` of `module_inject/replace_module.py:182` and the inference transformer it builds,
+`model_implementations/transformers/ds_bert.py` over `ops/transformer/inference/ds_attention.py`).
+
+Unlike decoders (converted whole into `DSInferenceModel` with a paged KV cache), an encoder has no cache and its
+embeddings / pooler / heads stay the HF modules: each encoder layer is swapped IN PLACE for a `DSEncoderLayer`
+that keeps the HF call contract (hidden_states, attention_mask, ...) -> hidden_states, so every task head
+(MaskedLM, SequenceClassification, QA, ...) keeps working.
+
+`DSEncoderLayer` (post-LN, the BERT family's layout):
+  qkv    = x . Wqkv^T + b                 one GEMM over the concatenated q|k|v weights (bias in the GEMM epilogue)
+  ctx    = SDPA(q, k, v, mask)            non-causal, padding mask as an additive / boolean bias
+  x1     = LN(ctx . Wo^T + bo + x)        GEMM (+bias epilogue), then the fused residual-add + LayerNorm kernel
+  h      = gelu(x1 . W1^T + b1)           GEMM, then the fused bias + GELU kernel
+  out    = LN(h . W2^T + b2 + x1)         GEMM (+bias epilogue), fused residual-add + LayerNorm
+Tensor parallelism shards q/k/v and W1 by output rows (heads / intermediate), Wo and W2 by input columns, with one
+all-reduce after each row-parallel GEMM (bias added once, after the reduction).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import comm as dist
+from ..ops.transformer import functional as DF
+
+_BERT_LIKE = ("BertLayer", "RobertaLayer", "XLMRobertaLayer", "ElectraLayer", "CamembertLayer", "RobertaPreLayerNormLayer")
+_DISTIL = ("TransformerBlock", )
+_ACTS = {"gelu": "gelu", "gelu_new": "gelu_tanh", "gelu_pytorch_tanh": "gelu_tanh", "relu": "relu", "silu": "silu"}
+
+
+def _is_bert_layer(m):
+    return type(m).__name__ in _BERT_LIKE and hasattr(m, "attention") and hasattr(m.attention, "self") \
+        and hasattr(m.attention.self, "query") and not getattr(m, "is_decoder", False)
+
+
+def _is_distil_block(m):
+    return type(m).__name__ in _DISTIL and hasattr(m, "attention") and hasattr(m.attention, "q_lin") \
+        and hasattr(m, "ffn")
+
+
+def supported(model):
+    return any(_is_bert_layer(m) or _is_distil_block(m) for m in model.modules())
+
+
+class DSEncoderLayer(nn.Module):
+
+    def __init__(self, q, k, v, o, ln1, w1, w2, ln2, num_heads, act, tp_group=None, tp_size=1, tp_rank=0,
+                 dtype=torch.bfloat16, device=None):
+        super().__init__()
+        H = q.weight.shape[1]
+        assert num_heads % tp_size == 0, "heads must divide the tensor-parallel size"
+        self.nh = num_heads // tp_size
+        self.hd = H // num_heads
+        self.tp_group, self.tp = tp_group, tp_size
+        self.act = _ACTS.get(act, "gelu")
+        self.eps1, self.eps2 = ln1.eps, ln2.eps
+        kw = dict(dtype=dtype, device=device)
+
+        def rows(t, r=tp_rank):
+            n = t.shape[0] // tp_size
+            return t[r * n:(r + 1) * n]
+
+        def cols(t, r=tp_rank):
+            n = t.shape[1] // tp_size
+            return t[:, r * n:(r + 1) * n]
+
+        def p(t):
+            return nn.Parameter(t.detach().to(**kw).contiguous(), requires_grad=False)
+
+        self.qkv_w = p(torch.cat([rows(q.weight), rows(k.weight), rows(v.weight)], 0))
+        self.qkv_b = p(torch.cat([rows(q.bias), rows(k.bias), rows(v.bias)], 0))
+        self.o_w, self.o_b = p(cols(o.weight)), p(o.bias)
+        self.ln1_w, self.ln1_b = p(ln1.weight), p(ln1.bias)
+        self.w1, self.b1 = p(rows(w1.weight)), p(rows(w1.bias))
+        self.w2, self.b2 = p(cols(w2.weight)), p(w2.bias)
+        self.ln2_w, self.ln2_b = p(ln2.weight), p(ln2.bias)
+
+    def _row_parallel(self, x, w, b):
+        if self.tp == 1:
+            return F.linear(x, w, b)
+        y = F.linear(x, w)
+        dist.all_reduce(y, group=self.tp_group)
+        return y + b
+
+    @staticmethod
+    def _mask(mask, dtype):
+        if mask is None:
+            return None
+        if mask.dim() == 2:  # [B, S] 1 = keep
+            mask = mask[:, None, None, :].bool()
+        if mask.dtype == torch.bool:
+            return mask
+        return mask.to(dtype)
+
+    def forward(self, hidden_states, attention_mask=None, *args, **kwargs):
+        x = hidden_states
+        B, S, _ = x.shape
+        qkv = F.linear(x, self.qkv_w, self.qkv_b).view(B, S, 3, self.nh, self.hd)
+        q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
+        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=self._mask(attention_mask, q.dtype))
+        ctx = ctx.transpose(1, 2).reshape(B, S, self.nh * self.hd)
+        a = self._row_parallel(ctx, self.o_w, self.o_b)
+        x1, _ = DF.layer_norm(a, self.ln1_w, self.ln1_b, self.eps1, residual=x)
+        h = DF.bias_activation(F.linear(x1, self.w1), self.b1, self.act)
+        f = self._row_parallel(h, self.w2, self.b2)
+        out, _ = DF.layer_norm(f, self.ln2_w, self.ln2_b, self.eps2, residual=x1)
+        return out
+
+
+def _from_bert(m, cfg, **kw):
+    a = m.attention
+    return DSEncoderLayer(a.self.query, a.self.key, a.self.value, a.output.dense, a.output.LayerNorm,
+                          m.intermediate.dense, m.output.dense, m.output.LayerNorm, cfg.num_attention_heads,
+                          getattr(cfg, "hidden_act", "gelu"), **kw)
+
+
+def _from_distil(m, cfg, **kw):
+    a = m.attention
+    return DSEncoderLayer(a.q_lin, a.k_lin, a.v_lin, a.out_lin, m.sa_layer_norm, m.ffn.lin1, m.ffn.lin2,
+                          m.output_layer_norm, getattr(cfg, "n_heads", None) or cfg.num_attention_heads,
+                          getattr(cfg, "activation", "gelu"), **kw)
+
+
+def inject(model, tp_group=None, tp_size=1, tp_rank=0, dtype=torch.bfloat16, device=None):
+    """Replace every encoder layer of `model` in place; the rest of the model is cast / moved to (dtype, device).
+    Returns the number of layers replaced."""
+    cfg = model.config
+    kw = dict(tp_group=tp_group, tp_size=tp_size, tp_rank=tp_rank, dtype=dtype, device=device)
+    n = 0
+    for parent in list(model.modules()):
+        for name, child in list(parent.named_children()):
+            if _is_bert_layer(child):
+                if getattr(child, "crossattention", None) is not None:
+                    continue  # cross-attention decoder layers keep the HF implementation
+                setattr(parent, name, _from_bert(child, cfg, **kw))
+                n += 1
+            elif _is_distil_block(child):
+                setattr(parent, name, _from_distil(child, cfg, **kw))
+                n += 1
+    model.to(device=device, dtype=dtype)
+    return n

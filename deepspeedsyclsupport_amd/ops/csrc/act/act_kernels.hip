@@ -139,6 +139,28 @@ __global__ void __launch_bounds__(256) bias_residual_kernel(const T* __restrict_
   }
 }
 
+// y = x + bias + other + other_bias over channels-last rows (spatial `nhwc_bias_add_bias_add`; diffusers UNet/VAE
+// residual joins). Either of (other, other_bias) may be null.
+template <typename T>
+__global__ void __launch_bounds__(256) bias_add2_kernel(const T* __restrict__ x, const T* __restrict__ bias,
+                                                        const T* __restrict__ other, const T* __restrict__ obias,
+                                                        T* __restrict__ y, int64_t rows, int C) {
+  const int64_t nvec_row = C / 8;
+  const int64_t total = rows * nvec_row;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t r = t / nvec_row, c = (t - r * nvec_row) * 8;
+    float v[8], b[8], o[8], ob[8];
+    Vec8<T>::load(x + r * C + c, v);
+    Vec8<T>::load(bias + c, b);
+    if (other) Vec8<T>::load(other + r * C + c, o);
+    if (obias) Vec8<T>::load(obias + c, ob);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += b[j] + (other ? o[j] : 0.f) + (obias ? ob[j] : 0.f);
+    Vec8<T>::store(y + r * C + c, v);
+  }
+}
+
 }  // namespace
 
 #define DISPATCH_T(dt, ...)                                    \
@@ -213,6 +235,17 @@ extern "C" int ds_bias_residual(const void* x, const void* bias, const void* res
   const int grid = ds_grid_for(rows * (C / 8), 256);
   DISPATCH_T(dtype, hipLaunchKernelGGL((bias_residual_kernel<T>), dim3(grid), dim3(256), 0, s, (const T*)x,
                                        (const T*)bias, (const T*)res, (T*)y, rows, C, res_scale));
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ds_bias_add2(const void* x, const void* bias, const void* other, const void* obias, void* y,
+                            int64_t rows, int C, int dtype, hipStream_t s) {
+  if (C % 8 || bias == nullptr) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
+  const int grid = ds_grid_for(rows * (C / 8), 256);
+  DISPATCH_T(dtype, hipLaunchKernelGGL((bias_add2_kernel<T>), dim3(grid), dim3(256), 0, s, (const T*)x,
+                                       (const T*)bias, (const T*)other, (const T*)obias, (T*)y, rows, C));
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -35,6 +35,7 @@ int ds_bias_act_bwd(const void*, const void*, const void*, void*, int64_t, int, 
 int ds_bias_residual(const void*, const void*, const void*, void*, int64_t, int, float, int, hipStream_t);
 int ds_dropout_fwd(const void*, const void*, const void*, void*, uint8_t*, int64_t, int, float, uint64_t, uint64_t, int,
                    hipStream_t);
+int ds_bias_add2(const void*, const void*, const void*, const void*, void*, int64_t, int, int, hipStream_t);
 int ds_dropout_bwd(const void*, void*, int64_t, int, float, uint64_t, uint64_t, int, hipStream_t);
 int ds_qkv_rope_fwd(const void*, void*, void*, void*, const float*, const float*, const int*, int, int, int, int, int,
                     int, int, const int64_t*, int, hipStream_t);
@@ -278,6 +279,20 @@ Tensor bias_residual(Tensor x, OptT bias, OptT res, double res_scale) {
   return y;
 }
 
+// x [..., C] channels-last: y = x + bias (+ other) (+ other_bias)
+Tensor bias_add2(Tensor x, Tensor bias, OptT other, OptT other_bias) {
+  need(x, "x");
+  const int C = (int)x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && bias.numel() == C && bias.scalar_type() == x.scalar_type(), "bias_add2: bias [C], C % 8");
+  if (other.has_value()) TORCH_CHECK(other->sizes() == x.sizes() && other->is_contiguous(), "other shape");
+  if (other_bias.has_value()) TORCH_CHECK(other_bias->numel() == C, "other_bias [C]");
+  auto y = torch::empty_like(x);
+  check(ds_bias_add2(x.data_ptr(), bias.data_ptr(), ptr_or_null(other), ptr_or_null(other_bias), y.data_ptr(),
+                     x.numel() / C, C, dcode(x), stream()),
+        "bias_add2");
+  return y;
+}
+
 // ------------------------------------------------------------------------------------------ dropout
 // y = res + dropout_p(x + bias); the keep mask is a pure function of (seed, offset, element) so the backward
 // regenerates it. want_mask returns the packed mask (bit j of byte t = element 8t + j) for tests.
@@ -455,6 +470,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("bias_residual", &bias_residual);
+  m.def("bias_add2", &bias_add2);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("qkv_rope_fwd", &qkv_rope_fwd, py::arg("qkv"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("hq"),

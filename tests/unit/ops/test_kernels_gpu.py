@@ -497,3 +497,17 @@ def test_dropout_autograd_and_checkpoint_replay():
     y2 = torch.utils.checkpoint.checkpoint(lambda t: DF.dropout(t, 0.2, True, bias=b, residual=r), x,
                                            use_reentrant=False)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+def test_spatial_nhwc_bias_add(dt):
+    from deepspeedsyclsupport_amd.ops import spatial
+    torch.manual_seed(2)
+    x = torch.randn(2, 320, 16, 16, device="cuda").to(dt).to(memory_format=torch.channels_last)
+    o = torch.randn(2, 320, 16, 16, device="cuda").to(dt).to(memory_format=torch.channels_last)
+    b, ob = torch.randn(320, device="cuda").to(dt), torch.randn(320, device="cuda").to(dt)
+    bb, obb = b.view(1, -1, 1, 1).float(), ob.view(1, -1, 1, 1).float()
+    torch.testing.assert_close(spatial.nhwc_bias_add(x, b).float(), x.float() + bb, **TOL[dt])
+    torch.testing.assert_close(spatial.nhwc_bias_add_add(x, b, o).float(), x.float() + bb + o.float(), **TOL[dt])
+    torch.testing.assert_close(spatial.nhwc_bias_add_bias_add(x, b, o, ob).float(),
+                               x.float() + bb + o.float() + obb, **TOL[dt])
