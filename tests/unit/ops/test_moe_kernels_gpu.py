@@ -57,13 +57,15 @@ def test_grouped_gemm(R, E, N, K):
     if E > 2:
         counts[1] += counts[2]  # an empty expert in the middle
         counts[2] = 0
-    y = moe_ops.grouped_gemm(x, w, counts)
+    y = moe_ops.hip_ops().grouped_gemm(x, w, counts)  # the in-tree MFMA kernel at every size
     ref = torch.empty(R, N, device="cuda")
     s = 0
     for e, c in enumerate(counts.tolist()):
         ref[s:s + c] = x[s:s + c].float() @ w[e].float().t()
         s += c
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    # size-dispatched entry (library grouped GEMM above GROUPED_LIBRARY_MIN_ROWS)
+    torch.testing.assert_close(moe_ops.grouped_gemm(x, w, counts).float(), ref, rtol=2e-2, atol=2e-2)
 
 
 @pytest.mark.parametrize("T,H,I,E,k", [(1, 256, 256, 8, 2), (200, 512, 384, 8, 2), (96, 256, 512, 16, 4)])
