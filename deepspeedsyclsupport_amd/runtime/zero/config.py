@@ -60,6 +60,8 @@ class DeepSpeedZeroConfig(DeepSpeedConfigModel):
     memory_efficient_linear: bool = True
     pipeline_loading_checkpoint: bool = False
     override_module_apply: bool = True
+    # debug mode: cross-rank consistency check before every ZeRO collective (runtime/zero/utils.py)
+    safe_mode: bool = False
 
     @model_validator(mode="after")
     def _fixups(self):

@@ -96,6 +96,9 @@ class ParamCoordinator:
         opt = self.opt
         if g.status != ZeroParamStatus.NOT_AVAILABLE:
             return
+        if opt.safe_mode and g.partition:
+            from .utils import assert_ints_same_as_other_ranks
+            assert_ints_same_as_other_ranks([g.idx, g.padded], g.dp_group, "parameter all-gather (group id, numel)")
         compute = self.acc.current_stream() if self.ag_stream is not None else None
         if self.ag_stream is not None:
             self.ag_stream.wait_stream(compute)
@@ -177,6 +180,10 @@ class ParamCoordinator:
     def reset_step(self):
         """End of an optimizer step: close the trace, release anything still gathered."""
         if self.mode == RECORD:
+            if self.opt.safe_mode and self.trace:
+                from .utils import assert_ints_same_as_other_ranks, trace_digest
+                assert_ints_same_as_other_ranks(trace_digest(self.trace), self.opt.dp_group,
+                                                "recorded ZeRO-3 fetch trace (length, digest)")
             self.mode = COMPLETE if self.trace else RECORD
         elif self.mode == INVALID:
             self.trace = []

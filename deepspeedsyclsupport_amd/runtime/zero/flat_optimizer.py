@@ -120,6 +120,7 @@ class FlatZeroOptimizer:
         self.module = module
         self.stage = int(stage)
         self.zc = zero_config
+        self.safe_mode = bool(zero_config is not None and getattr(zero_config, "safe_mode", False))
         self.cfg = ds_config
         self.dtype = dtype
         self.clip_grad = clip_grad
@@ -448,6 +449,10 @@ class FlatZeroOptimizer:
                 g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
             g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1))
             p.grad = None
+        if self.safe_mode and g.pending <= 0:
+            from .utils import ZeRORuntimeException
+            raise ZeRORuntimeException(f"fetch group {g.idx}: more gradients than parameters in one backward pass "
+                                       "(a parameter's gradient was produced twice)")
         g.pending -= 1
         if g.pending == 0 and g.mode != self.LOCAL and self._should_reduce_now():
             self._reduce_group(g)
@@ -474,6 +479,10 @@ class FlatZeroOptimizer:
         if g.reduced_this_pass:
             return
         g.reduced_this_pass = True
+        if self.safe_mode and not self._local_grads():
+            from .utils import assert_ints_same_as_other_ranks
+            assert_ints_same_as_other_ranks([g.idx, g.padded, int(g.partition)], g.dp_group,
+                                            "gradient reduction (group id, numel, partitioned)")
         src = g.grad_flat
         compute = self.acc.current_stream() if self.rs_stream is not None else None
         ctx = self.acc.stream(self.rs_stream) if self.rs_stream is not None else _nullctx()
