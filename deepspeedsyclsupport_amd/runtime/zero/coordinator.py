@@ -16,6 +16,7 @@ from ... import comm as dist
 from ...utils.logging import logger
 from .flat_optimizer import ZeroParamStatus
 from .linear import install_zero3_linear
+from ...utils.nvtx import instrument_w_nvtx
 
 RECORD, COMPLETE, INVALID = 0, 1, 2
 
@@ -92,6 +93,7 @@ class ParamCoordinator:
         if hpz is not None and not self.in_backward:
             hpz.keep_secondary(g)
 
+    @instrument_w_nvtx
     def _issue(self, g):
         opt = self.opt
         if g.status != ZeroParamStatus.NOT_AVAILABLE:
@@ -123,6 +125,7 @@ class ParamCoordinator:
             self.opt._point_params(g)
             g.status = ZeroParamStatus.AVAILABLE
 
+    @instrument_w_nvtx
     def fetch(self, g):
         self._trace(g)
         if g.status == ZeroParamStatus.NOT_AVAILABLE:
@@ -130,6 +133,7 @@ class ParamCoordinator:
         self._wait(g)
         self._prefetch()
 
+    @instrument_w_nvtx
     def release(self, g):
         if g.persistent or g.status == ZeroParamStatus.NOT_AVAILABLE:
             return

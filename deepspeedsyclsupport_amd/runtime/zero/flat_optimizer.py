@@ -40,6 +40,7 @@ from ...ops.adam.fused_adam import FusedAdam
 from ...utils.logging import log_dist, logger
 from ..fp16.loss_scaler import CreateLossScaler
 from .config import ZeroStageEnum
+from ...utils.nvtx import instrument_w_nvtx
 
 ALIGN = 64  # elements: keeps every rank segment 128-B (bf16) aligned for 16-B vector access
 
@@ -475,6 +476,7 @@ class FlatZeroOptimizer:
     def _prescale(self):
         return self.comm_dtype == torch.float16 and self._div() > 1
 
+    @instrument_w_nvtx
     def _reduce_group(self, g):
         if g.reduced_this_pass:
             return
@@ -550,6 +552,7 @@ class FlatZeroOptimizer:
             loss.backward(retain_graph=retain_graph)
         self.backward_epilogue()
 
+    @instrument_w_nvtx
     def backward_epilogue(self):
         """Flush groups whose params got no grad this pass (unused params count as zero) and join streams."""
         if self._should_reduce_now():
@@ -662,6 +665,7 @@ class FlatZeroOptimizer:
         return sq
 
     @torch.no_grad()
+    @instrument_w_nvtx
     def step(self, closure=None, lr_kwargs=None):
         """Optimizer step at the accumulation boundary (the engine only calls it there)."""
         items = self._grad_items()
@@ -707,6 +711,7 @@ class FlatZeroOptimizer:
         if self.device.type == "cuda":
             torch.cuda.current_stream().synchronize()
 
+    @instrument_w_nvtx
     def _device_step(self, items, grad_scale):
         adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
         if self._fused_adam:
@@ -771,6 +776,7 @@ class FlatZeroOptimizer:
             for (og, moff, n, gr, lp, s, _h) in items:
                 lp.copy_(self.master[og][moff:moff + n])
 
+    @instrument_w_nvtx
     def _host_step(self, grad_scale):
         """Twin-Flow host half: native CPU Adam on pinned fp32 partitions (runs on a worker thread, concurrently
         with the device Adam launched on the main thread)."""
