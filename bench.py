@@ -32,6 +32,9 @@ def parse():
     ap.add_argument("--gas", type=int, default=1)
     ap.add_argument("--stage", type=int, default=3)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing (not needed with 288 GB HBM)")
+    ap.add_argument("--sp", type=int, default=1,
+                    help="Ulysses sequence-parallel degree (BASELINE config: Llama-2 7B, seq 32k, sp over xGMI "
+                         "all-to-all); dp = world / sp")
     ap.add_argument("--local_rank", type=int, default=0)
     ap.add_argument("--host-dryrun", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank control flow (tiny model; not a measurement)")
@@ -143,10 +146,23 @@ def main():
             "stage3_max_live_parameters": int(3e9),
         },
     }
+    assert world % args.sp == 0, "--sp must divide the number of ranks"
+    dp = world // args.sp
+    if args.sp > 1:
+        config["sequence_parallel"] = {"size": args.sp}
+        config["train_batch_size"] = dp * args.micro_batch * args.gas
     engine, _, _, _ = ds.initialize(model=model, config=config)
+    sp_group = None
+    if args.sp > 1:
+        from deepspeedsyclsupport_amd.parallel import groups
+        from deepspeedsyclsupport_amd.sequence.layer import enable_sequence_parallel, shard_sequence
+        sp_group = groups._get_sequence_parallel_group()
+        n_sp = enable_sequence_parallel(engine.module, sp_group)
+        log(f"[bench] Ulysses sequence parallel sp={args.sp} dp={dp} on {n_sp} attention modules")
     log(f"[bench] engine ready in {time.time() - t0:.1f}s; mem {mem_gib():.1f} GiB")
 
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    # every rank of one sequence-parallel group must see the same sequences (it keeps its own 1/sp slice)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank // args.sp)
     # a distinct synthetic batch for every micro-step (no repeated data for the model to memorise)
     n_micro = (args.warmup + args.steps) * args.gas
     batches = [torch.randint(0, cfg.vocab_size, (args.micro_batch, args.seq_len), device=dev, generator=g)
@@ -155,7 +171,11 @@ def main():
     def train_step(i):
         for a in range(args.gas):
             x = batches[i * args.gas + a]
-            loss = engine(x, labels=x)
+            if sp_group is not None:
+                inp, lab, off = shard_sequence(x, x, sp_group)
+                loss = engine(inp, labels=lab, pos_offset=off, shift_labels=False)
+            else:
+                loss = engine(x, labels=x)
             engine.backward(loss)
             engine.step()
         return loss
@@ -181,7 +201,7 @@ def main():
     elapsed = float(t)
 
     ms_per_step = elapsed / args.steps * 1e3
-    tokens_per_step = world * args.micro_batch * args.gas * args.seq_len
+    tokens_per_step = dp * args.micro_batch * args.gas * args.seq_len  # each sp group covers whole sequences
     tok_s = tokens_per_step * args.steps / elapsed
     flops_tok = cfg.flops_per_token(args.seq_len)
     tflops_gpu = tok_s * flops_tok / world / 1e12
@@ -202,9 +222,9 @@ def main():
             "data": "synthetic (uniform random token ids, random-init weights)",
             "config": {
                 "model": {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "tiny": "llama-tiny"}[args.model],
-                "global_batch": world * args.micro_batch * args.gas,
+                "global_batch": dp * args.micro_batch * args.gas,
                 "seq_len": args.seq_len,
-                "parallelism": f"dp{world}",
+                "parallelism": f"dp{dp}" + (f"-sp{args.sp}" if args.sp > 1 else ""),
                 "zero_stage": args.stage,
                 "micro_batch_per_gpu": args.micro_batch,
                 "gradient_accumulation_steps": args.gas,
