@@ -17,6 +17,10 @@
 //    so HBM latency hides under the MFMA work; one barrier per tile;
 //  * causal: fully-masked tiles are skipped per wave, heavy query blocks are launched first, and the block->tile map
 //    keeps every (batch, head) on one XCD so its K/V stay in that XCD's L2.
+//  * block-sparse variant (SPARSE=true, reference `ops/sparse_attention` SDD/softmax/DSD Triton kernels): each
+//    workgroup walks only the 64-key tiles listed for its (layout head, 128-row query block) in a host-built LUT, and
+//    masks inside a tile at the layout's block granularity (16/32/64/128) with a per-lane 64-bit allow mask built
+//    from the block layout — compute and K/V traffic scale with the layout's density, not with S^2.
 // Outputs O (any [B,H,S,D] strides, e.g. written straight into the [B,S,H,D] layout the o_proj GEMM wants) and the
 // natural-log LSE [B,H,S] in fp32 that the backward pass consumes.
 #include "ds_hip.h"
@@ -44,12 +48,21 @@ __device__ __forceinline__ int lds_off(int row, int ch) {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <bool CAUSAL>
+// block-sparse LUT: tiles [lay_heads, nqb, max_tiles] (ascending 64-key tile ids), ntiles [lay_heads, nqb],
+// layout [lay_heads, nb, nb] (uint8, block granularity blk)
+struct SparseLut {
+  const int* tiles;
+  const int* ntiles;
+  const uint8_t* layout;
+  int max_tiles, lay_heads, nb, blk;
+};
+
+template <bool CAUSAL, bool SPARSE>
 __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V, bf16* __restrict__ O,
     float* __restrict__ LSE, int B, int Hq, int Hk, int S, int Skv, int64_t qsb, int64_t qsh, int64_t qss,
     int64_t ksb, int64_t ksh, int64_t kss, int64_t vsb, int64_t vsh, int64_t vss, int64_t osb, int64_t osh,
-    int64_t oss, float c /* softmax scale * log2(e) */, float scale) {
+    int64_t oss, float c /* softmax scale * log2(e) */, float scale, SparseLut lut) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
 
@@ -78,6 +91,13 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
 
   int nt = (Skv + BN - 1) / BN;
   if (CAUSAL) nt = min(nt, (q0 + BM + BN - 1) / BN);
+  const int lh = SPARSE ? (lut.lay_heads == 1 ? 0 : hq) : 0;
+  const int* tlist = nullptr;
+  if constexpr (SPARSE) {
+    nt = lut.ntiles[lh * nqb + qb];
+    tlist = lut.tiles + ((int64_t)lh * nqb + qb) * lut.max_tiles;
+  }
+  auto tile_of = [&](int j) { return SPARSE ? tlist[j] : j; };
 
   // LDS: [K0][K1][V0][V1][scratch]
   float* scratch = reinterpret_cast<float*>(smem + 4 * TILE_BYTES) + wid * 32;
@@ -110,14 +130,16 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
   float m_run = -INFINITY, l_run = 0.f;
   const int qrow_lane = q0w + l32;  // the query row this lane's scores belong to
 
-  stage_load(0);
-  stage_store(0);
+  if (nt > 0) {  // uniform per workgroup (a sparse row block may have no tiles)
+    stage_load(tile_of(0));
+    stage_store(0);
+  }
   __syncthreads();
 
   for (int j = 0; j < nt; ++j) {
     const int cur = j & 1;
-    if (j + 1 < nt) stage_load(j + 1);
-    const int k0 = j * BN;
+    if (j + 1 < nt) stage_load(tile_of(j + 1));
+    const int k0 = tile_of(j) * BN;
     const bool active = !CAUSAL || k0 <= q0w + 31;
     if (active) {
       const char* Kt = smem + cur * TILE_BYTES;
@@ -132,6 +154,26 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
         for (int kk = 0; kk < 8; ++kk) {
           const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(Kt + lds_off(t * 32 + l32, 2 * kk + h));
           s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[t], 0, 0, 0);
+        }
+      }
+      // ---------------- block-sparse mask at the layout's granularity (this lane's query row vs the 64 keys)
+      if constexpr (SPARSE) {
+        const int qr = min(qrow_lane, S - 1);
+        const uint8_t* lrow = lut.layout + ((int64_t)lh * lut.nb + qr / lut.blk) * lut.nb;
+        uint64_t allow = 0;
+        for (int kb = k0 / lut.blk; kb < lut.nb && kb * lut.blk < k0 + BN; ++kb) {
+          if (!lrow[kb]) continue;
+          const int lo = max(kb * lut.blk - k0, 0), hi = min((kb + 1) * lut.blk - k0, BN);
+          allow |= (hi - lo >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1)) << lo;
+        }
+        if (allow != ~0ull) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rel = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              if (!((allow >> rel) & 1ull)) s[t][r] = -INFINITY;
+            }
         }
       }
       // ---------------- masking (causal diagonal / ragged key tail)
@@ -249,20 +291,22 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
   (void)scale;
 }
 
-template <bool C>
+template <bool C, bool SP>
 int launch(const bf16* q, const bf16* k, const bf16* v, bf16* o, float* lse, int B, int Hq, int Hk, int S, int Skv,
-           const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os, float scale, hipStream_t st) {
+           const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os, float scale, hipStream_t st,
+           SparseLut lut = SparseLut{nullptr, nullptr, nullptr, 0, 1, 0, 1}) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_fwd_kernel<C>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_fwd_kernel<C, SP>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr = true;
   }
   const int nqb = (S + BM - 1) / BM;
   const int grid = nqb * B * Hq;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL((flash_fwd_kernel<C>), dim3(grid), dim3(NTHR), LDS_BYTES, st, q, k, v, o, lse, B, Hq, Hk, S, Skv,
-                     qs[0], qs[1], qs[2], ks[0], ks[1], ks[2], vs[0], vs[1], vs[2], os[0], os[1], os[2], c, scale);
+  hipLaunchKernelGGL((flash_fwd_kernel<C, SP>), dim3(grid), dim3(NTHR), LDS_BYTES, st, q, k, v, o, lse, B, Hq, Hk, S,
+                     Skv, qs[0], qs[1], qs[2], ks[0], ks[1], ks[2], vs[0], vs[1], vs[2], os[0], os[1], os[2], c, scale,
+                     lut);
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -279,6 +323,20 @@ extern "C" int ds_flash_fwd(const void* q, const void* k, const void* v, void* o
   auto k_ = (const bf16*)k;
   auto v_ = (const bf16*)v;
   auto o_ = (bf16*)o;
-  return causal ? launch<true>(q_, k_, v_, o_, lse, B, Hq, Hk, S, Skv, qs, ks, vs, os, scale, st)
-                : launch<false>(q_, k_, v_, o_, lse, B, Hq, Hk, S, Skv, qs, ks, vs, os, scale, st);
+  return causal ? launch<true, false>(q_, k_, v_, o_, lse, B, Hq, Hk, S, Skv, qs, ks, vs, os, scale, st)
+                : launch<false, false>(q_, k_, v_, o_, lse, B, Hq, Hk, S, Skv, qs, ks, vs, os, scale, st);
+}
+
+// Block-sparse forward: same tensors as ds_flash_fwd (non-causal; causality, if wanted, is part of the layout) plus
+// the LUT described at SparseLut. lay_heads is 1 (shared layout) or Hq. Requires S == Skv.
+extern "C" int ds_flash_fwd_sparse(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Hq,
+                                   int Hk, int S, const int64_t* qs, const int64_t* ks, const int64_t* vs,
+                                   const int64_t* os, float scale, const int* tiles, const int* ntiles,
+                                   const uint8_t* layout, int max_tiles, int lay_heads, int nb, int blk,
+                                   hipStream_t st) {
+  if (Hk <= 0 || Hq % Hk != 0 || S <= 0 || blk <= 0 || nb * blk < S || max_tiles < 0 ||
+      (lay_heads != 1 && lay_heads != Hq) || tiles == nullptr || ntiles == nullptr || layout == nullptr)
+    return (int)hipErrorInvalidValue;
+  return launch<false, true>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, Hq, Hk, S, S, qs, ks,
+                             vs, os, scale, st, SparseLut{tiles, ntiles, layout, max_tiles, lay_heads, nb, blk});
 }

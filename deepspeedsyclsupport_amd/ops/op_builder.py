@@ -233,8 +233,33 @@ _BUILDERS = {
     "CPULionBuilder": ("cpu_lion", "ds_cpu_ops"),
     "AsyncIOBuilder": ("async_io", "ds_cpu_ops"),
     "ShareMemCommBuilder": ("deepspeed_shm_comm", "ds_cpu_ops"),
+    "RandomLTDBuilder": ("random_ltd", "ds_hip_ops"),
+    "SpatialInferenceBuilder": ("spatial_inference", "ds_hip_ops"),
+    "SparseAttnBuilder": ("sparse_attn", "ds_hip_ops"),
+    "EvoformerAttnBuilder": ("evoformer_attn", "ds_hip_ops"),
+    "InferenceCutlassBuilder": ("cutlass_ops", "ds_hip_ops"),
+    "RaggedUtilsBuilder": ("ragged_ops", "ds_hip_ops"),
 }
 for _cls, (_name, _ext) in _BUILDERS.items():
     globals()[_cls] = _mk(_cls, _name, _ext)
 
+
+
+class UtilsBuilder(OpBuilder):
+    """Reference `csrc/utils/flatten_unflatten.cpp` (torch flatten wrappers): no native code is needed for that."""
+    NAME = "utils"
+
+    def is_compatible(self, verbose=False):
+        return True
+
+    def load(self, verbose=False):
+        import types
+
+        import torch._utils as tu
+        return types.SimpleNamespace(flatten=tu._flatten_dense_tensors, unflatten=tu._unflatten_dense_tensors)
+
+    jit_load = load
+
+
 ALL_OPS = {globals()[c].NAME: globals()[c] for c in _BUILDERS}
+ALL_OPS["utils"] = UtilsBuilder

@@ -1,10 +1,11 @@
 """Block-sparse self-attention (reference `ops/sparse_attention/sparse_self_attention.py`,
 `bert_sparse_self_attention.py`, `sparse_attention_utils.py`).
 
-The block layout from a SparsityConfig is expanded once per sequence length into a token-level additive mask
-(cached on device) and attention runs through the fused SDPA path with that mask; padding / attention masks in
-'add' or 'mul' mode are folded in. (The reference's Triton SDD/DSD kernels are replaced by the fused attention
-kernels; layouts and API are the same.)
+bf16 device inputs without extra masks run the block-sparse gfx950 flash kernel (`block_sparse.py`: only the key
+tiles the layout touches are visited). Otherwise the block layout is expanded once per sequence length into a
+token-level additive mask (cached on device) and attention runs through the fused SDPA path with that mask; padding
+/ attention masks in 'add' or 'mul' mode and relative position embeddings are folded in. Layouts and API are the
+reference's.
 """
 import torch
 import torch.nn as nn
@@ -25,7 +26,12 @@ class SparseSelfAttention(nn.Module):
         self._masks = {}
 
     def get_layout(self, L):
-        return self.sparsity_config.make_layout(L)
+        lay = self._layouts.get(L) if hasattr(self, "_layouts") else None
+        if lay is None:
+            if not hasattr(self, "_layouts"):
+                self._layouts = {}
+            lay = self._layouts[L] = self.sparsity_config.make_layout(L)
+        return lay
 
     def _block_mask(self, L, device):
         key = (L, str(device))
@@ -48,6 +54,10 @@ class SparseSelfAttention(nn.Module):
         B, H, L, D = query.shape
         if query.dtype not in (torch.float16, torch.bfloat16, torch.float32):
             raise TypeError("sparse attention supports fp16/bf16/fp32")
+        from . import block_sparse
+        blk = self.sparsity_config.block
+        if block_sparse.native_ok(query, key, value, blk, rpe, key_padding_mask, attn_mask):
+            return block_sparse.block_sparse_attention(query, key, value, self.get_layout(L), blk)
         bias = self._block_mask(L, query.device)[None]              # [1, H, L, L]
         if rpe is not None:
             bias = bias + rpe.float().view(-1, H, L, L) if rpe.dim() == 4 else bias + rpe.float()

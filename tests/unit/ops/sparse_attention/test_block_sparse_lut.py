@@ -1,0 +1,44 @@
+"""Host-side LUT of the block-sparse flash kernel: for every (layout head, 128-row query block) the listed 64-key
+tiles must be exactly the tiles holding at least one allowed key for at least one of the block's rows."""
+import pytest
+import torch
+
+from deepspeedsyclsupport_amd.ops.sparse_attention import block_sparse as bs
+from deepspeedsyclsupport_amd.ops.sparse_attention.sparsity_config import (BigBirdSparsityConfig,
+                                                                            BSLongformerSparsityConfig,
+                                                                            FixedSparsityConfig,
+                                                                            VariableSparsityConfig)
+
+
+@pytest.mark.parametrize("cfg", [
+    FixedSparsityConfig(num_heads=4, block=16, num_local_blocks=4),
+    FixedSparsityConfig(num_heads=4, block=64, num_local_blocks=2, attention="unidirectional"),
+    BigBirdSparsityConfig(num_heads=4, block=32),
+    BSLongformerSparsityConfig(num_heads=4, block=128),
+    VariableSparsityConfig(num_heads=4, block=32, different_layout_per_head=True),
+    BigBirdSparsityConfig(num_heads=2, block=256),
+], ids=["fixed16", "fixed64uni", "bigbird32", "longformer128", "variable_perhead", "bigbird256"])
+def test_lut_matches_brute_force(cfg):
+    L = 1024
+    lay = cfg.make_layout(L)
+    tiles, ntiles, lay_u8 = bs.build_lut(lay, cfg.block, L, "cpu")
+    LH = lay_u8.shape[0]
+    assert LH in (1, lay.shape[0])
+    tok = lay.bool().repeat_interleave(cfg.block, 1).repeat_interleave(cfg.block, 2)
+    for h in range(LH):
+        for qb in range(L // 128):
+            need = tok[h, qb * 128:(qb + 1) * 128].any(0).reshape(L // 64, 64).any(-1).nonzero().flatten().tolist()
+            got = tiles[h, qb, :ntiles[h, qb]].tolist()
+            assert got == need, (h, qb)
+    if LH == 1:
+        assert torch.equal(lay_u8[0].bool(), lay[0].bool())
+
+
+def test_token_bias_and_native_gate():
+    cfg = BigBirdSparsityConfig(num_heads=2, block=16)
+    lay = cfg.make_layout(256)
+    b = bs.token_bias(lay, 16, 256, 2, torch.float32, "cpu")
+    assert b.shape == (1, 2, 256, 256)
+    assert torch.equal(b[0] == 0, lay.bool().repeat_interleave(16, 1).repeat_interleave(16, 2))
+    q = torch.randn(1, 2, 256, 64)
+    assert not bs.native_ok(q, q, q, 16)  # host tensors never take the kernel path
