@@ -133,7 +133,9 @@ class FlatZeroOptimizer:
         self.acc = get_accelerator()
         self.device = torch.device(self.acc.device_name(self.acc.current_device())) if self.acc.device_name() != "cpu" \
             else torch.device("cpu")
-        self.partition = self.stage >= 1 and self.dp > 1
+        # DS_ZERO_FORCE_PARTITION=1 runs the partitioned code path (all-gather / reduce-scatter on the comm streams,
+        # shard pointing, qwZ/qgZ) even with one data-parallel rank: the single-GPU rehearsal of the multi-GPU path
+        self.partition = self.stage >= 1 and (self.dp > 1 or os.environ.get("DS_ZERO_FORCE_PARTITION", "0") == "1")
         self.world = dist.get_world_size()
         self._setup_mics()
         self.comm_dtype = communication_data_type or dtype

@@ -70,3 +70,22 @@ def test_param_offload_gpu_matches_device(pdev, opt_dev, tmp_path):
     ref = _engine(3, "fp32", 4, 3e-3)
     got = _engine(3, "fp32", 4, 3e-3, extra)
     assert got == pytest.approx(ref, rel=1e-4, abs=1e-4), (got, ref)
+
+
+@pytest.mark.parametrize("stage", [1, 2, 3])
+def test_partitioned_path_on_one_gpu(stage, monkeypatch):
+    """The multi-GPU code path (RCCL all-gather on the ag stream, reduce-scatter on the rs stream, shard pointing,
+    prefetch) forced on with a single rank: must still track torch.optim.AdamW."""
+    monkeypatch.setenv("DS_ZERO_FORCE_PARTITION", "1")
+    ref = _torch_ref(6, 3e-3)
+    got = _engine(stage, "fp32", 6, 3e-3, {"stage3_param_persistence_threshold": 0})
+    assert got == pytest.approx(ref, rel=2e-3, abs=2e-3), (got, ref)
+
+
+def test_partitioned_zeropp_on_one_gpu(monkeypatch):
+    """ZeRO++ qwZ (int8 weight all-gather) + qgZ (quantized gradient reduce-scatter) through the RCCL path."""
+    monkeypatch.setenv("DS_ZERO_FORCE_PARTITION", "1")
+    ref = _torch_ref(6, 3e-3)
+    got = _engine(3, "bf16", 6, 3e-3, {"stage3_param_persistence_threshold": 0, "zero_quantized_weights": True,
+                                       "zero_quantized_gradients": True})
+    assert got == pytest.approx(ref, rel=5e-2, abs=5e-2), (got, ref)
