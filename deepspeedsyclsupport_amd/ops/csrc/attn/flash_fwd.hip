@@ -53,6 +53,7 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 struct SparseLut {
   const int* tiles;
   const int* ntiles;
+  const int* qorder;  // [lay_heads, nqb] query blocks by descending tile count
   const uint8_t* layout;
   int max_tiles, lay_heads, nb, blk;
 };
@@ -70,10 +71,15 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
   const int nqb = (S + BM - 1) / BM;
   const int nwg = gridDim.x;
   const int logical = xcd_remap(blockIdx.x, nwg);
+  // (batch, head)-major so one head's query blocks share an XCD's L2 (K/V tiles reused across its query blocks);
+  // within a head the heaviest query blocks go first (causal: the longest rows; sparse: the LUT's order by tile
+  // count, so global-attention rows do not start last). Measured: query-block-major heavy-first order loses more
+  // to L2 misses than it gains in tail length (tools/bench_sparse_attn.py).
   const int bh = logical / nqb;
   const int qbi = logical % nqb;
-  const int qb = CAUSAL ? nqb - 1 - qbi : qbi;  // heaviest (longest causal row range) first
   const int b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hk);
+  const int lh = SPARSE ? (lut.lay_heads == 1 ? 0 : hq) : 0;
+  const int qb = SPARSE ? lut.qorder[lh * nqb + qbi] : (CAUSAL ? nqb - 1 - qbi : qbi);  // heaviest first
   const int q0 = qb * BM, q0w = q0 + wid * 32;
 
   const bf16* Qp = Q + b * qsb + hq * qsh;
@@ -91,7 +97,6 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
 
   int nt = (Skv + BN - 1) / BN;
   if (CAUSAL) nt = min(nt, (q0 + BM + BN - 1) / BN);
-  const int lh = SPARSE ? (lut.lay_heads == 1 ? 0 : hq) : 0;
   const int* tlist = nullptr;
   if constexpr (SPARSE) {
     nt = lut.ntiles[lh * nqb + qb];
@@ -294,7 +299,7 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
 template <bool C, bool SP>
 int launch(const bf16* q, const bf16* k, const bf16* v, bf16* o, float* lse, int B, int Hq, int Hk, int S, int Skv,
            const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os, float scale, hipStream_t st,
-           SparseLut lut = SparseLut{nullptr, nullptr, nullptr, 0, 1, 0, 1}) {
+           SparseLut lut = SparseLut{nullptr, nullptr, nullptr, nullptr, 0, 1, 0, 1}) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_fwd_kernel<C, SP>),
@@ -332,11 +337,13 @@ extern "C" int ds_flash_fwd(const void* q, const void* k, const void* v, void* o
 extern "C" int ds_flash_fwd_sparse(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Hq,
                                    int Hk, int S, const int64_t* qs, const int64_t* ks, const int64_t* vs,
                                    const int64_t* os, float scale, const int* tiles, const int* ntiles,
-                                   const uint8_t* layout, int max_tiles, int lay_heads, int nb, int blk,
-                                   hipStream_t st) {
+                                   const int* qorder, const uint8_t* layout, int max_tiles, int lay_heads, int nb,
+                                   int blk, hipStream_t st) {
   if (Hk <= 0 || Hq % Hk != 0 || S <= 0 || blk <= 0 || nb * blk < S || max_tiles < 0 ||
-      (lay_heads != 1 && lay_heads != Hq) || tiles == nullptr || ntiles == nullptr || layout == nullptr)
+      (lay_heads != 1 && lay_heads != Hq) || tiles == nullptr || ntiles == nullptr || qorder == nullptr ||
+      layout == nullptr)
     return (int)hipErrorInvalidValue;
   return launch<false, true>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, Hq, Hk, S, S, qs, ks,
-                             vs, os, scale, st, SparseLut{tiles, ntiles, layout, max_tiles, lay_heads, nb, blk});
+                             vs, os, scale, st,
+                             SparseLut{tiles, ntiles, qorder, layout, max_tiles, lay_heads, nb, blk});
 }

@@ -46,8 +46,8 @@ int ds_rope_inplace(void*, int, int, int, int, int64_t, int64_t, int64_t, const 
 int ds_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*,
                  const int64_t*, const int64_t*, const int64_t*, float, int, hipStream_t);
 int ds_flash_fwd_sparse(const void*, const void*, const void*, void*, float*, int, int, int, int, const int64_t*,
-                        const int64_t*, const int64_t*, const int64_t*, float, const int*, const int*, const uint8_t*,
-                        int, int, int, int, hipStream_t);
+                        const int64_t*, const int64_t*, const int64_t*, float, const int*, const int*, const int*,
+                        const uint8_t*, int, int, int, int, hipStream_t);
 int ds_xent_fwd(const void*, const int64_t*, float*, float*, int64_t, int, int64_t, int, float, int, hipStream_t);
 int ds_xent_bwd(const void*, const int64_t*, const float*, const float*, float, void*, int64_t, int, int64_t, int64_t,
                 int, float, int, hipStream_t);
@@ -449,7 +449,7 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, double 
 // Block-sparse flash forward (non-causal; causality belongs to the layout). tiles int32 [LH, nqb, T], ntiles int32
 // [LH, nqb], layout uint8 [LH, nb, nb] at granularity blk; LH in {1, Hq}. Same q/k/v/o/lse contract as flash_fwd.
 std::vector<Tensor> flash_fwd_sparse(Tensor q, Tensor k, Tensor v, double scale, Tensor tiles, Tensor ntiles,
-                                     Tensor layout, int64_t blk, bool want_lse) {
+                                     Tensor qorder, Tensor layout, int64_t blk, bool want_lse) {
   TORCH_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "flash_fwd_sparse: device tensors expected");
   TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "flash_fwd_sparse: 4-D [B,H,S,D] tensors expected");
   TORCH_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 && v.scalar_type() == at::kBFloat16,
@@ -461,13 +461,15 @@ std::vector<Tensor> flash_fwd_sparse(Tensor q, Tensor k, Tensor v, double scale,
   TORCH_CHECK(Hq % Hk == 0, "flash_fwd_sparse: Hq must be a multiple of Hk");
   for (const Tensor* t : {&q, &k, &v})
     for (int d = 0; d < 3; ++d) TORCH_CHECK(t->stride(d) % 8 == 0, "flash_fwd_sparse: strides must be multiples of 8");
-  need(tiles, "tiles"); need(ntiles, "ntiles"); need(layout, "layout");
+  need(tiles, "tiles"); need(ntiles, "ntiles"); need(layout, "layout"); need(qorder, "qorder");
   TORCH_CHECK(tiles.scalar_type() == at::kInt && ntiles.scalar_type() == at::kInt && layout.scalar_type() == at::kByte,
               "flash_fwd_sparse: int32 tiles/ntiles, uint8 layout");
   const int64_t LH = layout.size(0), nb = layout.size(1), nqb = (S + 127) / 128;
   TORCH_CHECK(layout.dim() == 3 && layout.size(2) == nb && nb * blk >= S, "flash_fwd_sparse: layout [LH, nb, nb]");
   TORCH_CHECK((LH == 1 || LH == Hq) && tiles.dim() == 3 && tiles.size(0) == LH && tiles.size(1) == nqb &&
-                  ntiles.numel() == LH * nqb, "flash_fwd_sparse: LUT shape");
+                  ntiles.numel() == LH * nqb && qorder.numel() == LH * nqb && qorder.scalar_type() == at::kInt,
+              "flash_fwd_sparse: LUT shape");
+  TORCH_CHECK(qorder.min().item<int>() >= 0 && qorder.max().item<int>() < nqb, "flash_fwd_sparse: qorder range");
   // every listed tile must lie inside the key range (the kernel trusts the LUT for its K/V addresses)
   if (tiles.numel() > 0)
     TORCH_CHECK(tiles.min().item<int>() >= 0 && tiles.max().item<int>() < (S + 63) / 64 &&
@@ -480,7 +482,7 @@ std::vector<Tensor> flash_fwd_sparse(Tensor q, Tensor k, Tensor v, double scale,
                 vs[3] = {v.stride(0), v.stride(1), v.stride(2)}, os[3] = {o.stride(0), o.stride(1), o.stride(2)};
   check(ds_flash_fwd_sparse(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
                             want_lse ? lse.data_ptr<float>() : nullptr, (int)B, (int)Hq, (int)Hk, (int)S, qs, ks, vs,
-                            os, (float)scale, tiles.data_ptr<int>(), ntiles.data_ptr<int>(),
+                            os, (float)scale, tiles.data_ptr<int>(), ntiles.data_ptr<int>(), qorder.data_ptr<int>(),
                             layout.data_ptr<uint8_t>(), (int)tiles.size(2), (int)LH, (int)nb, (int)blk, stream()),
         "flash_fwd_sparse");
   return {o, lse};

@@ -24,7 +24,8 @@ def _lut_key(layout, blk, L, device):
 
 
 def build_lut(layout, blk, L, device):
-    """layout [H, nb, nb] (0/1) -> (tiles int32 [LH, nqb, T], ntiles int32 [LH, nqb], layout uint8 [LH, nb, nb]).
+    """layout [H, nb, nb] (0/1) -> (tiles int32 [LH, nqb, T], ntiles int32 [LH, nqb], layout uint8 [LH, nb, nb],
+    qorder int32 [LH, nqb] = query blocks by descending tile count, the kernel's launch order).
 
     LH = 1 when every head shares one layout. Tile t of query block qb is listed when any key of 64-key tile t is
     allowed for any of the 128 query rows of qb; the tile lists are ascending."""
@@ -44,8 +45,9 @@ def build_lut(layout, blk, L, device):
     ntiles = t64.sum(-1).to(torch.int32)
     T = max(int(ntiles.max()), 1)
     order = torch.sort((~t64).to(torch.int8), dim=-1, stable=True).indices[..., :T].to(torch.int32)
+    qorder = torch.sort(ntiles, dim=-1, descending=True, stable=True).indices.to(torch.int32)  # heaviest first
     lut = (order.contiguous().to(device), ntiles.contiguous().to(device),
-           lay.to(torch.uint8).contiguous().to(device))
+           lay.to(torch.uint8).contiguous().to(device), qorder.contiguous().to(device))
     if len(_LUTS) > 64:
         _LUTS.clear()
     _LUTS[key] = lut
@@ -66,14 +68,15 @@ class BlockSparseAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, layout, blk, scale):
         B, H, L, D = q.shape
-        tiles, ntiles, lay_u8 = build_lut(layout, blk, L, q.device)
+        tiles, ntiles, lay_u8, qorder = build_lut(layout, blk, L, q.device)
         if D < 128:
             pad = (0, 128 - D)
             qp, kp, vp = (torch.nn.functional.pad(t, pad) for t in (q, k, v))
         else:
             qp, kp, vp = q, k, v
         need_grad = any(t.requires_grad for t in (q, k, v))
-        o, lse = hip_ops().flash_fwd_sparse(qp, kp, vp, float(scale), tiles, ntiles, lay_u8, int(blk), need_grad)
+        o, lse = hip_ops().flash_fwd_sparse(qp, kp, vp, float(scale), tiles, ntiles, qorder, lay_u8, int(blk),
+                                              need_grad)
         if D < 128:
             # keep the [B, L, H, D] memory layout the kernel wrote: the efficient-attention backward reads O with
             # that layout (a [B, H, L, D]-contiguous O gives wrong dK/dV and can fault — tools/probe_sparse_bwd.py)

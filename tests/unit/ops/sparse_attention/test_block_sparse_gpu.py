@@ -61,5 +61,5 @@ def test_sparse_self_attention_module_uses_kernel():
     o = attn(q, k, v)
     ref = _dense_ref(q, k, v, attn.get_layout(L), 64, D**-0.5)
     torch.testing.assert_close(o.float(), ref, rtol=2e-2, atol=2e-2)
-    tiles, ntiles, _ = bs.build_lut(attn.get_layout(L), 64, L, q.device)
+    tiles, ntiles, _, _ = bs.build_lut(attn.get_layout(L), 64, L, q.device)
     assert ntiles.float().mean().item() < 0.5 * (L // 64)  # the kernel really skips most key tiles

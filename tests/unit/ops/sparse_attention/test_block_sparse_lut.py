@@ -21,7 +21,9 @@ from deepspeedsyclsupport_amd.ops.sparse_attention.sparsity_config import (BigBi
 def test_lut_matches_brute_force(cfg):
     L = 1024
     lay = cfg.make_layout(L)
-    tiles, ntiles, lay_u8 = bs.build_lut(lay, cfg.block, L, "cpu")
+    tiles, ntiles, lay_u8, qorder = bs.build_lut(lay, cfg.block, L, "cpu")
+    assert sorted(qorder[0].tolist()) == list(range(L // 128))
+    assert all(ntiles[0, qorder[0, i]] >= ntiles[0, qorder[0, i + 1]] for i in range(L // 128 - 1))
     LH = lay_u8.shape[0]
     assert LH in (1, lay.shape[0])
     tok = lay.bool().repeat_interleave(cfg.block, 1).repeat_interleave(cfg.block, 2)

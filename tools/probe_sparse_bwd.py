@@ -22,9 +22,9 @@ qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
 ref = torch.softmax((qr @ kr.transpose(-1, -2)) * scale + bias32, -1) @ vr
 do = torch.randn_like(ref)
 ref.backward(do)
-tiles, ntiles, lay = bs.build_lut(layout, 16, L, q.device)
+tiles, ntiles, lay, qorder = bs.build_lut(layout, 16, L, q.device)
 pad = lambda t: torch.nn.functional.pad(t, (0, 128 - D))
-o, lse = hip_ops().flash_fwd_sparse(pad(q), pad(k), pad(v), scale, tiles, ntiles, lay, 16, True)
+o, lse = hip_ops().flash_fwd_sparse(pad(q), pad(k), pad(v), scale, tiles, ntiles, qorder, lay, 16, True)
 o = o[..., :D].contiguous()
 print("fwd err", (o.float() - ref).abs().max().item())
 z = torch.zeros((), dtype=torch.int64, device="cuda")
