@@ -161,6 +161,22 @@ class DSInferenceLayer(nn.Module):
             getattr(self, name).data = torch.empty(0, dtype=getattr(self, name).dtype,
                                                    device=getattr(self, name).device)
 
+    def _linear(self, x, name, bias=None):
+        """x . W^T (+ bias). Int8 weight-only layers at decode sizes (<= 4 token rows) run the fused-dequant skinny
+        kernel (`csrc/gemv/skinny_int8.hip`: streams int8 + group scales, never materialises a bf16 weight);
+        everything else dequantises into a bf16 temporary for a library GEMM (reference `ds_vector_matmul_int8`)."""
+        qw = self.quant.get(name)
+        if qw is not None and x.is_cuda and x.dtype == torch.bfloat16 and qw.qt.bits == 8 \
+                and qw.qt.zeros.numel() == 0 and len(qw.shape) == 2:
+            from ...ops.native import hip_ops
+            K = x.shape[-1]
+            M = x.numel() // K
+            if hip_ops().skinny_i8_ok(M, K, qw.qt.group_size):
+                y = hip_ops().skinny_i8(x.reshape(M, K).contiguous(), qw.qt.data, qw.qt.scales, bias, qw.shape[0],
+                                        qw.qt.group_size)
+                return y.view(*x.shape[:-1], qw.shape[0])
+        return F.linear(x, self._w(name), bias)
+
     def _w(self, name):
         return self.quant[name].materialize() if name in self.quant else getattr(self, name)
 
@@ -213,8 +229,8 @@ class DSInferenceLayer(nn.Module):
         return o.reshape(B, n, self.hq * D)
 
     def _attention(self, x, meta: BatchMeta, cache, rope, alibi):
-        qkv = F.linear(x, self._w("qkv_w"), self.qkv_b)
-        out = F.linear(self._attend(qkv, meta, cache, rope, alibi), self._w("o_w"))
+        qkv = self._linear(x, "qkv_w", self.qkv_b)
+        out = self._linear(self._attend(qkv, meta, cache, rope, alibi), "o_w")
         out = self._allreduce(out)
         if self.o_b is not None:
             out = out + self.o_b
@@ -237,12 +253,12 @@ class DSInferenceLayer(nn.Module):
     def _mlp(self, x):
         if self.spec.num_experts:
             return self._moe(x)
-        h = F.linear(x, self._w("fc1_w"), self.fc1_b)
+        h = self._linear(x, "fc1_w", self.fc1_b)
         if self.spec.gated_mlp:
             h = DF.gated_activation(h, self.spec.act)
         else:
             h = DF.bias_activation(h, None, self.spec.act)
-        out = F.linear(h, self._w("fc2_w"))
+        out = self._linear(h, "fc2_w")
         out = self._allreduce(out)
         if self.fc2_b is not None:
             out = out + self.fc2_b

@@ -21,6 +21,8 @@ int ds_paged_decode(const void*, const void*, const void*, const int*, const int
                     int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int ds_kv_append(const void*, const void*, void*, void*, const int*, const int*, int, int, int, int, int, int,
                  hipStream_t);
+int ds_skinny_i8_ok(int, int, int);
+int ds_skinny_i8(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
 int ds_quantize(const void*, int8_t*, float*, float*, int64_t, int, int, int, int, unsigned, int, hipStream_t);
 int ds_dequantize(const int8_t*, const float*, const float*, void*, int64_t, int, int, int, int, hipStream_t);
 int ds_dequant_reduce(const int8_t*, const float*, void*, int64_t, int, int, float, int, hipStream_t);
@@ -216,7 +218,34 @@ std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, 
   return {q};
 }
 
+bool skinny_i8_ok(int64_t M, int64_t K, int64_t gs) { return ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0; }
+
+// x [M, K] bf16 (M <= 4), q int8 [N * K] (row-major [N, K], symmetric), scales fp32 [N * K / gs] -> y [M, N] bf16
+Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_t gs) {
+  need(x, "x"); need(q, "q"); need(scales, "scales");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "skinny_i8: x must be bf16 [M, K]");
+  TORCH_CHECK(q.scalar_type() == at::kChar && scales.scalar_type() == at::kFloat, "skinny_i8: int8 q, fp32 scales");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(ds_skinny_i8_ok((int)M, (int)K, (int)gs), "skinny_i8: M <= 4, K % 16 == 0, gs % 16 == 0, K % gs == 0");
+  TORCH_CHECK(q.numel() == N * K && scales.numel() == N * K / gs, "skinny_i8: q / scales size");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_i8: 16-B aligned x / q");
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    need(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kBFloat16, "skinny_i8: bias bf16 [N]");
+    bp = bias->data_ptr();
+  }
+  auto y = torch::empty({M, N}, x.options());
+  check(ds_skinny_i8(x.data_ptr(), q.data_ptr<int8_t>(), scales.data_ptr<float>(), bp, y.data_ptr(), (int)M, (int)N,
+                     (int)K, (int)gs, stream()),
+        "skinny_i8");
+  return y;
+}
+
 void register_inference_ops(pybind11::module& m) {
+  m.def("skinny_i8_ok", &skinny_i8_ok);
+  m.def("skinny_i8", &skinny_i8);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_force_valu", &skinny_force_valu);
   m.def("skinny_set_path", &skinny_set_path);

@@ -44,6 +44,7 @@ EXTENSIONS = {
             "quant/quant_kernels.hip",
             "gemv/skinny_gemm.hip",
             "gemv/skinny_mfma.hip",
+            "gemv/skinny_int8.hip",
             "moe/moe_kernels.hip",
         ],
         "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp", "bind/moe_bind.cpp", "bind/host_mem.cpp"],

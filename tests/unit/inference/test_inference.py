@@ -211,3 +211,25 @@ def test_decode_graph_matches_eager_gpu():
     b = e2.generate(ids, max_new_tokens=12)
     assert e2.cuda_graph_created
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["llama", "bloom"])
+def test_int8_decode_gpu(kind):
+    """Weight-only int8 on the GPU: decode steps (<= 4 rows) take the fused-dequant skinny kernel, prefill the
+    dequantise + GEMM path; greedy tokens and last-token logits must follow the bf16 engine."""
+    import copy
+
+    import deepspeedsyclsupport_amd as ds
+    m = tiny(kind, H=256).eval()
+    ids = _ids(B=2, S=12).cuda()
+    e16 = ds.init_inference(copy.deepcopy(m), dtype=torch.bfloat16, replace_with_kernel_inject=True)
+    e8 = ds.init_inference(copy.deepcopy(m), dtype=torch.bfloat16, replace_with_kernel_inject=True,
+                           quant={"enabled": True, "weight": {"num_bits": 8}})
+    assert e8.module.layers[0].quant, "weights were not quantised"
+    g16 = e16.generate(ids, max_new_tokens=6)
+    l16 = e16(g16[:, :-1]).logits[:, -1].float()
+    l8 = e8(g16[:, :-1]).logits[:, -1].float()
+    assert (l8 - l16).abs().max().item() < 0.05 * l16.abs().max().item() + 0.05
+    g8 = e8.generate(ids, max_new_tokens=6)
+    assert g8.shape == g16.shape

@@ -511,3 +511,21 @@ def test_spatial_nhwc_bias_add(dt):
     torch.testing.assert_close(spatial.nhwc_bias_add_add(x, b, o).float(), x.float() + bb + o.float(), **TOL[dt])
     torch.testing.assert_close(spatial.nhwc_bias_add_bias_add(x, b, o, ob).float(),
                                x.float() + bb + o.float() + obb, **TOL[dt])
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("N,K,gs", [(1, 64, 64), (13, 4096, 64), (4096, 11008, 64), (1000, 14336, 128), (300, 57344, 64)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_skinny_int8_gemv(M, N, K, gs, bias):
+    """Weight-only int8 decode GEMV (fused group dequant) vs an fp32 GEMM on the dequantised weight."""
+    from deepspeedsyclsupport_amd.ops.quantizer import dequantize, quantize
+    torch.manual_seed(N + K)
+    w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+    qt = quantize(w, group_size=gs, bits=8, symmetric=True)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, device="cuda").bfloat16() if bias else None
+    y = ops().skinny_i8(x, qt.data, qt.scales, b, N, gs)
+    ref = x.float() @ dequantize(qt, torch.float32).t()
+    if bias:
+        ref = ref + b.float()
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * max(1.0, ref.abs().max().item()))
