@@ -162,7 +162,7 @@ class DSInferenceLayer(nn.Module):
                                                    device=getattr(self, name).device)
 
     def _linear(self, x, name, bias=None):
-        """x . W^T (+ bias). Int8 weight-only layers at decode sizes (<= 4 token rows) run the fused-dequant skinny
+        """x . W^T (+ bias). Int8 weight-only layers at decode sizes (<= 8 token rows) run the fused-dequant skinny
         kernel (`csrc/gemv/skinny_int8.hip`: streams int8 + group scales, never materialises a bf16 weight);
         everything else dequantises into a bf16 temporary for a library GEMM (reference `ds_vector_matmul_int8`)."""
         qw = self.quant.get(name)

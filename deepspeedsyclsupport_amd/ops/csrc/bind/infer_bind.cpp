@@ -220,13 +220,13 @@ std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, 
 
 bool skinny_i8_ok(int64_t M, int64_t K, int64_t gs) { return ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0; }
 
-// x [M, K] bf16 (M <= 4), q int8 [N * K] (row-major [N, K], symmetric), scales fp32 [N * K / gs] -> y [M, N] bf16
+// x [M, K] bf16 (M <= 8), q int8 [N * K] (row-major [N, K], symmetric), scales fp32 [N * K / gs] -> y [M, N] bf16
 Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_t gs) {
   need(x, "x"); need(q, "q"); need(scales, "scales");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "skinny_i8: x must be bf16 [M, K]");
   TORCH_CHECK(q.scalar_type() == at::kChar && scales.scalar_type() == at::kFloat, "skinny_i8: int8 q, fp32 scales");
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(ds_skinny_i8_ok((int)M, (int)K, (int)gs), "skinny_i8: M <= 4, K % 16 == 0, gs % 16 == 0, K % gs == 0");
+  TORCH_CHECK(ds_skinny_i8_ok((int)M, (int)K, (int)gs), "skinny_i8: M <= 8, K % 16 == 0, gs % 16 == 0, K % gs == 0");
   TORCH_CHECK(q.numel() == N * K && scales.numel() == N * K / gs, "skinny_i8: q / scales size");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
               "skinny_i8: 16-B aligned x / q");

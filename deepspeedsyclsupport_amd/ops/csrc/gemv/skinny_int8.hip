@@ -1,4 +1,4 @@
-// Weight-only int8 skinny GEMM for decode: y[M, N] = X[M, K] . (Q[N, K] * s[N, K / gs])^T (+ bias), M <= 4.
+// Weight-only int8 skinny GEMM for decode: y[M, N] = X[M, K] . (Q[N, K] * s[N, K / gs])^T (+ bias), M <= 8.
 //
 // Reference counterparts (behaviour, not code): the weight-only int8 inference path of `transformer_inference`
 // (`ds_vector_matmul_int8` / `dequantize_kernel`, `csrc/transformer/inference/csrc/pt_binding.cpp:13xx`,
@@ -11,7 +11,7 @@
 //    per row per step: one 16-byte non-temporal load per row; the group scale of that chunk (groups of >= 16
 //    elements along K, the quantiser's layout) is one fp32 load;
 //  * UNR chunks are issued before any is consumed (4 rows x UNR x 16 B in flight per lane) to cover HBM latency;
-//  * X (M <= 4 rows) is staged once per workgroup into LDS as bf16 when it fits (<= 64 KB), else read through L2;
+//  * X (M <= 8 rows) is staged once per workgroup into LDS as bf16 when it fits (<= 64 KB), else read through L2;
 //  * int8 -> f32 by byte extract + convert, fp32 FMA, one wave reduction per (row, token) at the end.
 #include "ds_hip.h"
 
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) skinny_i8_kernel(const bf16* __restrict__
 }  // namespace
 
 extern "C" int ds_skinny_i8_ok(int M, int K, int gs) {
-  return M >= 1 && M <= 4 && K % 16 == 0 && gs >= 16 && gs % 16 == 0 && K % gs == 0;
+  return M >= 1 && M <= 8 && K % 16 == 0 && gs >= 16 && gs % 16 == 0 && K % gs == 0;
 }
 
 // X [M, K] bf16, Q int8 [N, K] row-major, S fp32 [N * K / gs], bias bf16 [N] or null -> Y [M, N] bf16
@@ -125,22 +125,29 @@ extern "C" int ds_skinny_i8(const void* X, const int8_t* Q, const float* S, cons
   const int grid = min((quads + 3) / 4, 256 * 8);
   static bool attr = false;
   if (!attr) {
-    const void* ks[4] = {reinterpret_cast<const void*>(&skinny_i8_kernel<1>),
+    const void* ks[8] = {reinterpret_cast<const void*>(&skinny_i8_kernel<1>),
                          reinterpret_cast<const void*>(&skinny_i8_kernel<2>),
                          reinterpret_cast<const void*>(&skinny_i8_kernel<3>),
-                         reinterpret_cast<const void*>(&skinny_i8_kernel<4>)};
+                         reinterpret_cast<const void*>(&skinny_i8_kernel<4>),
+                         reinterpret_cast<const void*>(&skinny_i8_kernel<5>),
+                         reinterpret_cast<const void*>(&skinny_i8_kernel<6>),
+                         reinterpret_cast<const void*>(&skinny_i8_kernel<7>),
+                         reinterpret_cast<const void*>(&skinny_i8_kernel<8>)};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, XLDS_LIMIT);
     attr = true;
   }
   auto xb = (const bf16*)X;
   auto bb = (const bf16*)bias;
   auto yb = (bf16*)Y;
+#define DS_I8_CASE(MMV)                                                                                      \
+  case MMV:                                                                                                  \
+    hipLaunchKernelGGL(skinny_i8_kernel<MMV>, dim3(grid), dim3(256), shm, st, xb, Q, S, bb, yb, N, K, gs, xlds); \
+    break;
   switch (M) {
-    case 1: hipLaunchKernelGGL(skinny_i8_kernel<1>, dim3(grid), dim3(256), shm, st, xb, Q, S, bb, yb, N, K, gs, xlds); break;
-    case 2: hipLaunchKernelGGL(skinny_i8_kernel<2>, dim3(grid), dim3(256), shm, st, xb, Q, S, bb, yb, N, K, gs, xlds); break;
-    case 3: hipLaunchKernelGGL(skinny_i8_kernel<3>, dim3(grid), dim3(256), shm, st, xb, Q, S, bb, yb, N, K, gs, xlds); break;
-    default: hipLaunchKernelGGL(skinny_i8_kernel<4>, dim3(grid), dim3(256), shm, st, xb, Q, S, bb, yb, N, K, gs, xlds); break;
+    DS_I8_CASE(1) DS_I8_CASE(2) DS_I8_CASE(3) DS_I8_CASE(4) DS_I8_CASE(5) DS_I8_CASE(6) DS_I8_CASE(7)
+    default: hipLaunchKernelGGL(skinny_i8_kernel<8>, dim3(grid), dim3(256), shm, st, xb, Q, S, bb, yb, N, K, gs, xlds);
   }
+#undef DS_I8_CASE
   DS_CHECK_LAUNCH();
   return 0;
 }

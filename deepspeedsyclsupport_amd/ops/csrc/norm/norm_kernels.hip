@@ -335,7 +335,18 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
     else { constexpr int NV = 16; __VA_ARGS__; }                 \
   } while (0)
 
-static constexpr int kMaxHidden = 8192;
+// forward-only buckets for very wide rows (BLOOM-176B: 14336): one wave still owns a whole row, up to 256 fp32
+// values per lane in registers (one wave per SIMD at that size; the row-per-wave structure avoids a block reduction)
+#define DISPATCH_NV_FWD(H, ...)                                  \
+  do {                                                           \
+    const int nvf__ = ((H) + 511) / 512;                         \
+    if (nvf__ <= 16) { DISPATCH_NV(H, __VA_ARGS__); }            \
+    else if (nvf__ <= 24) { constexpr int NV = 24; __VA_ARGS__; } \
+    else { constexpr int NV = 32; __VA_ARGS__; }                 \
+  } while (0)
+
+static constexpr int kMaxHidden = 8192;      // backward kernels
+static constexpr int kMaxHiddenFwd = 16384;  // forward kernels
 static int norm_grid(int64_t rows) { return ds_grid_for((rows + 3) / 4, 1, 256 * 8); }
 
 // Number of fp32 partial rows the backward writes for `rows`. The host allocates part[(nb + 32) * H] for RMSNorm
@@ -344,11 +355,11 @@ extern "C" int ds_norm_bwd_blocks(int64_t rows) { return ds_grid_for((rows + 3) 
 
 extern "C" int ds_rms_fwd(const void* x, const void* r, const void* w, void* y, void* res_out, float* rstd,
                           int64_t rows, int H, float eps, int dtype, hipStream_t s) {
-  if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (H % 8 != 0 || H > kMaxHiddenFwd) return (int)hipErrorInvalidValue;
   if (r && !res_out) return (int)hipErrorInvalidValue;  // the fused-residual kernel always writes x + r
   if (rows <= 0) return 0;
   const int grid = norm_grid(rows);
-  DISPATCH_T(dtype, DISPATCH_NV(H, {
+  DISPATCH_T(dtype, DISPATCH_NV_FWD(H, {
     if (r)
       hipLaunchKernelGGL((rms_fwd_kernel<T, NV, true>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)r,
                          (const T*)w, (T*)y, (T*)res_out, rstd, rows, H, eps);
@@ -382,11 +393,11 @@ extern "C" int ds_rms_bwd(const void* dy, const void* x, const void* w, const fl
 
 extern "C" int ds_ln_fwd(const void* x, const void* r, const void* g, const void* b, void* y, void* res_out,
                          float* mean, float* rstd, int64_t rows, int H, float eps, int dtype, hipStream_t s) {
-  if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
+  if (H % 8 != 0 || H > kMaxHiddenFwd) return (int)hipErrorInvalidValue;
   if (r && !res_out) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
   const int grid = norm_grid(rows);
-  DISPATCH_T(dtype, DISPATCH_NV(H, {
+  DISPATCH_T(dtype, DISPATCH_NV_FWD(H, {
     if (r)
       hipLaunchKernelGGL((ln_fwd_kernel<T, NV, true>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)r,
                          (const T*)g, (const T*)b, (T*)y, (T*)res_out, mean, rstd, rows, H, eps);

@@ -36,9 +36,21 @@ class _RMSNormFn(torch.autograd.Function):
         return dx, dw, None, (dx if ctx.has_res else None)
 
 
+_NORM_BWD_MAX_H = 8192    # norm kernels: forward up to 16384 wide rows, backward up to 8192
+
+
+def _norm_kernel_ok(x, *params):
+    if not x.is_cuda or x.shape[-1] % 8:
+        return False
+    if x.shape[-1] <= _NORM_BWD_MAX_H:
+        return True
+    needs_grad = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (x, ) + params)
+    return x.shape[-1] <= 16384 and not needs_grad
+
+
 def rms_norm(x, weight, eps=1e-6, residual=None):
     """y = RMSNorm(x [+ residual]) * weight. With `residual`, returns (y, x + residual)."""
-    if x.is_cuda:
+    if _norm_kernel_ok(x, weight, residual):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -68,7 +80,7 @@ class _LayerNormFn(torch.autograd.Function):
 
 
 def layer_norm(x, weight, bias, eps=1e-5, residual=None):
-    if x.is_cuda and x.shape[-1] % 8 == 0:
+    if _norm_kernel_ok(x, weight, bias, residual):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()

@@ -216,7 +216,7 @@ def test_decode_graph_matches_eager_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["llama", "bloom"])
 def test_int8_decode_gpu(kind):
-    """Weight-only int8 on the GPU: decode steps (<= 4 rows) take the fused-dequant skinny kernel, prefill the
+    """Weight-only int8 on the GPU: decode steps (<= 8 rows) take the fused-dequant skinny kernel, prefill the
     dequantise + GEMM path; greedy tokens and last-token logits must follow the bf16 engine."""
     import copy
 

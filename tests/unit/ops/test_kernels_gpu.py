@@ -513,7 +513,7 @@ def test_spatial_nhwc_bias_add(dt):
                                x.float() + bb + o.float() + obb, **TOL[dt])
 
 
-@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("M", [1, 2, 4, 5, 8])
 @pytest.mark.parametrize("N,K,gs", [(1, 64, 64), (13, 4096, 64), (4096, 11008, 64), (1000, 14336, 128), (300, 57344, 64)])
 @pytest.mark.parametrize("bias", [False, True])
 def test_skinny_int8_gemv(M, N, K, gs, bias):
@@ -529,3 +529,25 @@ def test_skinny_int8_gemv(M, N, K, gs, bias):
     if bias:
         ref = ref + b.float()
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * max(1.0, ref.abs().max().item()))
+
+
+@pytest.mark.parametrize("H", [14336, 16384])
+@pytest.mark.parametrize("res", [False, True])
+def test_wide_norm_forward(H, res):
+    """Forward LayerNorm / RMSNorm on BLOOM-176B-wide rows (wide NV buckets) vs fp32 references."""
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(H)
+    x = torch.randn(5, H, device="cuda").bfloat16()
+    r = torch.randn(5, H, device="cuda").bfloat16() if res else None
+    g = torch.randn(H, device="cuda").bfloat16()
+    b = torch.randn(H, device="cuda").bfloat16()
+    h = x.float() + (r.float() if res else 0)
+    with torch.no_grad():
+        y = DF.layer_norm(x, g, b, 1e-5, r)
+        y = y[0] if res else y
+        yr = DF.rms_norm(x, g, 1e-6, r)
+        yr = yr[0] if res else yr
+    ref = F.layer_norm(h, (H, ), g.float(), b.float(), 1e-5)
+    ref_r = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
+    torch.testing.assert_close(y.float(), ref, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(yr.float(), ref_r, rtol=3e-2, atol=3e-2)
