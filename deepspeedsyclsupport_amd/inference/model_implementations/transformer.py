@@ -162,8 +162,9 @@ class DSInferenceLayer(nn.Module):
                                                    device=getattr(self, name).device)
 
     def _linear(self, x, name, bias=None):
-        """x . W^T (+ bias). Int8 weight-only layers at decode sizes (<= 8 token rows) run the fused-dequant skinny
-        kernel (`csrc/gemv/skinny_int8.hip`: streams int8 + group scales, never materialises a bf16 weight);
+        """x . W^T (+ bias). Int8 weight-only layers at decode sizes (<= 16 token rows) run the fused-dequant skinny
+        kernels (`csrc/gemv/skinny_int8.hip`: stream int8 + group scales into VALU FMAs for one row, into MFMAs
+        for 2-16 rows; never materialise a bf16 weight);
         everything else dequantises into a bf16 temporary for a library GEMM (reference `ds_vector_matmul_int8`)."""
         qw = self.quant.get(name)
         if qw is not None and x.is_cuda and x.dtype == torch.bfloat16 and qw.qt.bits == 8 \

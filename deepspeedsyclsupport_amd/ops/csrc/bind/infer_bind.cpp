@@ -22,6 +22,8 @@ int ds_paged_decode(const void*, const void*, const void*, const int*, const int
 int ds_kv_append(const void*, const void*, void*, void*, const int*, const int*, int, int, int, int, int, int,
                  hipStream_t);
 int ds_skinny_i8_ok(int, int, int);
+int ds_skinny_i8_mfma_ok(int, int, int);
+int ds_skinny_i8_mfma(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
 int ds_skinny_i8(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
 int ds_quantize(const void*, int8_t*, float*, float*, int64_t, int, int, int, int, unsigned, int, hipStream_t);
 int ds_dequantize(const int8_t*, const float*, const float*, void*, int64_t, int, int, int, int, hipStream_t);
@@ -218,15 +220,23 @@ std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, 
   return {q};
 }
 
-bool skinny_i8_ok(int64_t M, int64_t K, int64_t gs) { return ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0; }
+bool skinny_i8_ok(int64_t M, int64_t K, int64_t gs) {
+  return ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0 || ds_skinny_i8_mfma_ok((int)M, (int)K, (int)gs) != 0;
+}
 
 // x [M, K] bf16 (M <= 8), q int8 [N * K] (row-major [N, K], symmetric), scales fp32 [N * K / gs] -> y [M, N] bf16
-Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_t gs) {
+Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_t gs, int64_t path) {
   need(x, "x"); need(q, "q"); need(scales, "scales");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "skinny_i8: x must be bf16 [M, K]");
   TORCH_CHECK(q.scalar_type() == at::kChar && scales.scalar_type() == at::kFloat, "skinny_i8: int8 q, fp32 scales");
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(ds_skinny_i8_ok((int)M, (int)K, (int)gs), "skinny_i8: M <= 8, K % 16 == 0, gs % 16 == 0, K % gs == 0");
+  // path: 1 = VALU stream (M <= 8), 2 = MFMA (M <= 16, K and gs multiples of 64); 0 = pick (VALU up to 3 rows)
+  const bool valu_ok = ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0;
+  const bool mfma_ok = ds_skinny_i8_mfma_ok((int)M, (int)K, (int)gs) != 0;
+  // measured (tools/bench_int8_gemv.py): VALU 6.1-6.4 TB/s at 1 row, ~3 at 4 rows; MFMA ~3 TB/s flat to 8 rows
+  const bool use_mfma = path == 2 || (path == 0 && mfma_ok && (M > 3 || !valu_ok));
+  TORCH_CHECK(use_mfma ? mfma_ok : valu_ok, "skinny_i8: unsupported shape for the requested path (M ", M, ", K ", K,
+              ", gs ", gs, ")");
   TORCH_CHECK(q.numel() == N * K && scales.numel() == N * K / gs, "skinny_i8: q / scales size");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
               "skinny_i8: 16-B aligned x / q");
@@ -237,15 +247,21 @@ Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_
     bp = bias->data_ptr();
   }
   auto y = torch::empty({M, N}, x.options());
-  check(ds_skinny_i8(x.data_ptr(), q.data_ptr<int8_t>(), scales.data_ptr<float>(), bp, y.data_ptr(), (int)M, (int)N,
-                     (int)K, (int)gs, stream()),
-        "skinny_i8");
+  if (use_mfma)
+    check(ds_skinny_i8_mfma(x.data_ptr(), q.data_ptr<int8_t>(), scales.data_ptr<float>(), bp, y.data_ptr(), (int)M,
+                            (int)N, (int)K, (int)gs, stream()),
+          "skinny_i8_mfma");
+  else
+    check(ds_skinny_i8(x.data_ptr(), q.data_ptr<int8_t>(), scales.data_ptr<float>(), bp, y.data_ptr(), (int)M,
+                       (int)N, (int)K, (int)gs, stream()),
+          "skinny_i8");
   return y;
 }
 
 void register_inference_ops(pybind11::module& m) {
   m.def("skinny_i8_ok", &skinny_i8_ok);
-  m.def("skinny_i8", &skinny_i8);
+  m.def("skinny_i8", &skinny_i8, py::arg("x"), py::arg("q"), py::arg("scales"), py::arg("bias"), py::arg("N"),
+        py::arg("gs"), py::arg("path") = 0);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_force_valu", &skinny_force_valu);
   m.def("skinny_set_path", &skinny_set_path);
