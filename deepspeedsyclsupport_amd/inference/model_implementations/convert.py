@@ -113,6 +113,30 @@ def _gpt2(model):
     return spec, top, layers
 
 
+def _gpt_neo(model):
+    """GPT-Neo (reference container `module_inject/containers/gptneo.py`): learned positions, un-scaled attention
+    scores, alternating global / local (sliding-window) attention layers, biasless q/k/v."""
+    cfg = model.config
+    H, nh = cfg.hidden_size, cfg.num_heads
+    windows = tuple(cfg.window_size if t == "local" else 0 for t in cfg.attention_layers)
+    spec = DSModelSpec(arch="gpt_neo", vocab_size=cfg.vocab_size, hidden_size=H, num_layers=cfg.num_layers,
+                       num_heads=nh, num_kv_heads=nh, intermediate_size=cfg.intermediate_size or 4 * H, norm="ln",
+                       norm_eps=cfg.layer_norm_epsilon, pos="learned", act=cfg.activation_function, gated_mlp=False,
+                       qkv_bias=False, o_bias=True, mlp_bias=True, max_positions=cfg.max_position_embeddings,
+                       tie_embeddings=True, layer_windows=windows, attn_scale=1.0)
+    tr = model.transformer
+    layers = []
+    for L in tr.h:
+        at, mlp = L.attn.attention, L.mlp
+        layers.append(dict(ln1_w=L.ln_1.weight, ln1_b=L.ln_1.bias, ln2_w=L.ln_2.weight, ln2_b=L.ln_2.bias,
+                           q_w=at.q_proj.weight, k_w=at.k_proj.weight, v_w=at.v_proj.weight,
+                           o_w=at.out_proj.weight, o_b=at.out_proj.bias, fc1_w=mlp.c_fc.weight, fc1_b=mlp.c_fc.bias,
+                           fc2_w=mlp.c_proj.weight, fc2_b=mlp.c_proj.bias))
+    top = dict(embed=tr.wte.weight, pos_embed=tr.wpe.weight, norm_w=tr.ln_f.weight, norm_b=tr.ln_f.bias,
+               lm_head=model.lm_head.weight)
+    return spec, top, layers
+
+
 def _bloom(model):
     cfg = model.config
     H, nh = cfg.hidden_size, cfg.n_head
@@ -332,7 +356,7 @@ def _phi(model):
 CONVERTERS = {
     "llama": _llama_like, "mistral": _llama_like, "qwen2": _llama_like, "internlm": _llama_like,
     "gpt2": _gpt2, "bloom": _bloom, "opt": _opt, "gpt_neox": _gpt_neox, "gptj": _gptj,
-    "mixtral": _mixtral, "falcon": _falcon, "phi": _phi,
+    "mixtral": _mixtral, "falcon": _falcon, "phi": _phi, "gpt_neo": _gpt_neo,
 }
 
 

@@ -53,6 +53,8 @@ class DSModelSpec:
     max_positions: int = 4096
     learned_pos_offset: int = 0      # OPT uses 2
     sliding_window: int = 0
+    layer_windows: tuple = ()        # per-layer sliding windows (GPT-Neo local/global layers); () -> sliding_window
+    attn_scale: float = 0.0          # softmax scale; 0 -> 1/sqrt(head_dim) (GPT-Neo uses 1.0)
     lm_head_bias: bool = False
     num_experts: int = 0             # > 0: MoE MLP (Mixtral-style top-k router over gated experts)
     moe_top_k: int = 2
@@ -220,13 +222,14 @@ class DSInferenceLayer(nn.Module):
                 DF.apply_rotary_pos_emb(k, rope[0], rope[1], position_ids=pos, rotary_dim=spec.rotary_dim,
                                         interleaved=inter)
             _kv_append(k, v, kc, vc, meta)
-        scale = 1.0 / math.sqrt(D)
+        scale = spec.attn_scale or 1.0 / math.sqrt(D)
+        window = spec.layer_windows[self.layer_idx] if spec.layer_windows else spec.sliding_window
         if meta.prefill_from_zero and n > 1:
-            o = _prefill_attention(q, k, v, scale, alibi, spec.sliding_window)
+            o = _prefill_attention(q, k, v, scale, alibi, window)
         elif n == 1:
-            o = _decode_attention(q.view(B, self.hq, D), kc, vc, meta, scale, alibi, spec.sliding_window)
+            o = _decode_attention(q.view(B, self.hq, D), kc, vc, meta, scale, alibi, window)
         else:
-            o = _cached_attention(q, kc, vc, meta, scale, alibi, spec.sliding_window)
+            o = _cached_attention(q, kc, vc, meta, scale, alibi, window)
         return o.reshape(B, n, self.hq * D)
 
     def _attention(self, x, meta: BatchMeta, cache, rope, alibi):

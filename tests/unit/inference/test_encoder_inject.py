@@ -32,6 +32,14 @@ def tiny(kind, H=64, heads=4):
         c = T.DistilBertConfig(vocab_size=V, dim=H, n_layers=2, n_heads=heads, hidden_dim=4 * H,
                                max_position_embeddings=64)
         return T.DistilBertForMaskedLM(c)
+    if kind == "clip_text":
+        c = T.CLIPTextConfig(vocab_size=V, hidden_size=H, num_hidden_layers=2, num_attention_heads=heads,
+                             intermediate_size=4 * H, max_position_embeddings=64, eos_token_id=2)
+        return T.CLIPTextModel(c)
+    if kind == "clip_vision":
+        c = T.CLIPVisionConfig(hidden_size=H, num_hidden_layers=2, num_attention_heads=heads, intermediate_size=4 * H,
+                               image_size=32, patch_size=8)
+        return T.CLIPVisionModel(c)
     raise ValueError(kind)
 
 
@@ -46,6 +54,29 @@ def _inputs(B=3, S=17):
 
 def _out(o):
     return o.logits if hasattr(o, "logits") else o[0]
+
+
+@pytest.mark.parametrize("kind", ["clip_text", "clip_vision"])
+def test_clip_inject_parity_cpu(kind):
+    import deepspeedsyclsupport_amd as ds
+    m = tiny(kind).eval()
+    if kind == "clip_text":
+        ids, mask = _inputs()
+        kw = dict(input_ids=ids, attention_mask=mask)
+    else:
+        kw = dict(pixel_values=torch.randn(2, 3, 32, 32, generator=torch.Generator().manual_seed(3)))
+    with torch.no_grad():
+        ref = m(**kw)
+    eng = ds.init_inference(copy.deepcopy(m), dtype=torch.float32, replace_with_kernel_inject=True)
+    assert eng.encoder_injected == 2
+    with torch.no_grad():
+        out = eng(**kw)
+    a, b = out.last_hidden_state, ref.last_hidden_state
+    if kind == "clip_text":
+        valid = kw["attention_mask"].bool()
+        a, b = a[valid], b[valid]
+    assert (a - b).abs().max().item() < 1e-4
+    assert (out.pooler_output - ref.pooler_output).abs().max().item() < 1e-4
 
 
 @pytest.mark.parametrize("kind", ["bert", "bert_cls", "roberta", "distilbert"])
@@ -87,7 +118,7 @@ def test_encoder_inject_tp2(kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["bert", "roberta", "distilbert"])
+@pytest.mark.parametrize("kind", ["bert", "roberta", "distilbert", "clip_text"])
 def test_encoder_inject_bf16_gpu(kind):
     import deepspeedsyclsupport_amd as ds
     m = tiny(kind, H=256, heads=4).eval()

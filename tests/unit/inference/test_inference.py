@@ -31,6 +31,10 @@ def tiny(kind, H=64):
         c = T.Qwen2Config(vocab_size=V, hidden_size=H, intermediate_size=2 * H, num_hidden_layers=2,
                           num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=128)
         return T.Qwen2ForCausalLM(c)
+    if kind == "gpt_neo":
+        return T.GPTNeoForCausalLM(T.GPTNeoConfig(vocab_size=V, hidden_size=H, num_layers=4, num_heads=4,
+                                                  attention_types=[[["global", "local"], 2]], window_size=5,
+                                                  max_position_embeddings=128, bos_token_id=0, eos_token_id=1))
     if kind == "gpt2":
         return T.GPT2LMHeadModel(T.GPT2Config(vocab_size=V, n_embd=H, n_layer=2, n_head=4, n_positions=128,
                                               bos_token_id=0, eos_token_id=1))
@@ -68,7 +72,7 @@ def tiny(kind, H=64):
 
 
 ARCHS = ["llama", "mistral", "qwen2", "gpt2", "bloom", "opt", "gpt_neox", "gptj", "mixtral", "falcon", "falcon_new",
-         "falcon_seq", "phi"]
+         "falcon_seq", "phi", "gpt_neo"]
 
 
 def _ids(B=2, S=12, seed=1):
@@ -170,7 +174,7 @@ def _tp_run(kind, inject):
         assert torch.equal(eng.generate(ids, max_new_tokens=4), g_ref)
 
 
-@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt2", "mixtral", "falcon", "falcon_new", "phi"])
+@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt2", "mixtral", "falcon", "falcon_new", "phi", "gpt_neo"])
 def test_tp2_injected(kind):
     run_distributed(_tp_run, 2, kind, True)
 
@@ -182,7 +186,7 @@ def test_tp2_autotp(kind):
 
 # ---------------------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt_neox", "mixtral", "falcon", "phi"])
+@pytest.mark.parametrize("kind", ["llama", "bloom", "gpt_neox", "mixtral", "falcon", "phi", "gpt_neo"])
 def test_injected_bf16_gpu(kind):
     import deepspeedsyclsupport_amd as ds
     m = tiny(kind, H=256).eval()
