@@ -204,11 +204,20 @@ class InferenceEngine(torch.nn.Module):
         probs = logits.softmax(-1)
         return torch.multinomial(probs, 1, generator=generator).squeeze(-1)
 
+    def _moe_capturable(self, ids):
+        """MoE layers capture only on the device routing path (the reference fallback reads counts on the host)."""
+        if not self.module.spec.num_experts:
+            return True
+        from ..ops import moe_ops
+        probe = torch.empty(ids.shape[0], self.module.spec.hidden_size, dtype=self.dtype, device=self.device)
+        return all(moe_ops.native_moe_ok(probe, l.router_w, l.fc1_w, l.fc2_w, l.spec.moe_top_k)
+                   for l in self.module.layers)
+
     def _decode_step(self, ids, bt, lens, max_len):
         """One decode step for every sequence (ids [B, 1]); uses a captured HIP graph when enabled."""
         B = ids.shape[0]
         graphable = (self._config.enable_cuda_graph and self.device.type == "cuda" and self.dtype == torch.bfloat16
-                     and self.module.spec.head_dim in (64, 128, 256) and not self.module.spec.num_experts)
+                     and self.module.spec.head_dim in (64, 128, 256) and self._moe_capturable(ids))
         if not graphable:  # the gather-based fallback attention syncs with the host and cannot be captured
             meta = self._meta(bt, lens, 1, max_len)
             return self.module(ids, meta)
