@@ -135,7 +135,8 @@ class FlatZeroOptimizer:
             else torch.device("cpu")
         # DS_ZERO_FORCE_PARTITION=1 runs the partitioned code path (all-gather / reduce-scatter on the comm streams,
         # shard pointing, qwZ/qgZ) even with one data-parallel rank: the single-GPU rehearsal of the multi-GPU path
-        self.partition = self.stage >= 1 and (self.dp > 1 or os.environ.get("DS_ZERO_FORCE_PARTITION", "0") == "1")
+        self.force_partition = os.environ.get("DS_ZERO_FORCE_PARTITION", "0") == "1"
+        self.partition = self.stage >= 1 and (self.dp > 1 or self.force_partition)
         self.world = dist.get_world_size()
         self._setup_mics()
         self.comm_dtype = communication_data_type or dtype
@@ -187,7 +188,7 @@ class FlatZeroOptimizer:
         self._build_master()
         self._install_grad_hooks()
         self.coordinator = None
-        if self.stage == 3 and (self.dp > 1 or self.offload_param):
+        if self.stage == 3 and (self.dp > 1 or self.offload_param or self.force_partition):
             from .coordinator import ParamCoordinator
             self.coordinator = ParamCoordinator(self, prefetch_bucket_size=self.zc.prefetch_bucket_size,
                                                 max_live_parameters=self.zc.max_live_parameters)
@@ -225,8 +226,8 @@ class FlatZeroOptimizer:
         if self.stage == 3:
             # one group per module that directly owns trainable params (fetch granularity = module), plus ONE
             # persistent group for every small param (< param_persistence_threshold): never released.
-            thr = self.zc.param_persistence_threshold if (self.dp > 1 or self.offload_param) else 0
-            fetched = self.dp > 1 or self.offload_param  # groups gathered / streamed in per module
+            fetched = self.dp > 1 or self.offload_param or self.force_partition  # gathered / streamed per module
+            thr = self.zc.param_persistence_threshold if fetched else 0
             owned = set()
             persistent = []
             for name, m in self.module.named_modules():
@@ -264,8 +265,9 @@ class FlatZeroOptimizer:
             og = self.param_to_og[id(d["params"][0])]
             pg = self.og_dp_group[og]
             gdp, grank = dist.get_world_size(pg), dist.get_rank(pg)
-            persistent = d["persistent"] or (gdp == 1 and not self.offload_param)
-            g = FlatGroup(i, d["params"], gdp, grank, self.stage >= 1 and gdp > 1, persistent,
+            multi = gdp > 1 or self.force_partition
+            persistent = d["persistent"] or (not multi and not self.offload_param)
+            g = FlatGroup(i, d["params"], gdp, grank, self.stage >= 1 and multi, persistent,
                           self.device, self.dtype, d["module"], dp_group=pg)
             self.groups.append(g)
         self.param_group = {}
@@ -408,7 +410,7 @@ class FlatZeroOptimizer:
     LOCAL, PRESET, COPY = 0, 1, 2
 
     def _mode(self, g):
-        if g.reduce_dp == 1:
+        if g.reduce_dp == 1 and not self.force_partition:
             return self.LOCAL
         return self.PRESET if self.stage <= 1 else self.COPY
 
