@@ -1,10 +1,11 @@
 """Attention dispatch for training and prefill.
 
-On MI355X (bf16, head dim 128, no explicit mask / dropout) the forward runs the in-tree CDNA4 flash-attention kernel
-(`csrc/attn/flash_fwd.hip`: MFMA 32x32x16, swapped QK^T with in-register online softmax, transposed-LDS V reads).
-Its output memory is laid out [B, S, H, D], so the caller's `o.transpose(1, 2).reshape(B, S, H*D)` is free. The
-backward reuses the memory-efficient SDPA backward kernel, fed with our (O, LSE) pair — the kernel's contract is
-exactly (q, k, v, o, natural-log LSE [B,H,S]) (`tools/probe_attn_bwd.py` checks the interchange on the GPU).
+On MI355X (bf16, head dim 128, no explicit mask / dropout) both passes run in-tree CDNA4 kernels:
+ * forward `csrc/attn/flash_fwd.hip` (MFMA 32x32x16, swapped QK^T with in-register online softmax, transposed-LDS V
+   reads). Its output memory is laid out [B, S, H, D], so the caller's `o.transpose(1, 2).reshape(B, S, H*D)` is free;
+ * backward `csrc/attn/flash_bwd.hip`: one workgroup per 256 keys of one (batch, kv head) sweeping every query head
+   of the GQA group (no repeat_interleave of K/V, no dK/dV reduction), P recomputed from the forward's LSE, dQ by
+   f32 atomics. dq/dk/dv come back in the same [B, S, H, D] memory layout.
 
 Everything else (other head dims, masks, dropout, fp16/fp32, host tensors) goes through torch SDPA with the
 memory-efficient backend preferred (measured on MI355X: 451 TF fwd+bwd causal at B4·H32·S4096·D128 vs 243 TF for
@@ -40,18 +41,8 @@ def _sdpa(q, k, v, causal, scale, attn_mask=None, dropout_p=0.0):
     return F.scaled_dot_product_attention(q, k, v, **kw)
 
 
-_ZEROS = {}
-
-
-def _zero_seed(device):
-    z = _ZEROS.get(device)
-    if z is None:
-        z = _ZEROS[device] = torch.zeros((), dtype=torch.int64, device=device)
-    return z
-
-
 class FlashAttnFunc(torch.autograd.Function):
-    """Forward: gfx950 flash kernel (O, LSE). Backward: efficient-attention backward on that (O, LSE)."""
+    """Forward and backward on the gfx950 flash kernels (csrc/attn/flash_{fwd,bwd}.hip)."""
 
     @staticmethod
     def forward(ctx, q, k, v, causal, scale):
@@ -65,19 +56,11 @@ class FlashAttnFunc(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
+        from .native import hip_ops
         q, k, v, o, lse = ctx.saved_tensors
-        hq, hk = q.shape[1], k.shape[1]
-        rep = hq // hk
-        ke = k.repeat_interleave(rep, dim=1) if rep > 1 else k
-        ve = v.repeat_interleave(rep, dim=1) if rep > 1 else v
-        z = _zero_seed(q.device)  # no dropout: philox seed/offset unused
-        do = do if do.stride(-1) == 1 else do.contiguous()
-        dq, dk, dv, _ = torch.ops.aten._scaled_dot_product_efficient_attention_backward(
-            do, q, ke, ve, None, o, lse, z, z, 0.0, [True, True, True, False], ctx.causal, scale=ctx.scale)
-        if rep > 1:
-            B, _, S, D = dk.shape
-            dk = dk.view(B, hk, rep, S, D).sum(2)
-            dv = dv.view(B, hk, rep, S, D).sum(2)
+        if do.stride(-1) != 1 or any(s % 8 for s in do.stride()[:3]) or do.data_ptr() % 16:
+            do = do.contiguous()
+        dq, dk, dv = hip_ops().flash_bwd(q, k, v, o, lse, do, ctx.scale, 1 if ctx.causal else 0)
         return dq, dk, dv, None, None
 
 
@@ -85,7 +68,8 @@ def flash_supported(q, k, v, attn_mask=None, dropout_p=0.0):
     return (_USE_FLASH and q.is_cuda and attn_mask is None and dropout_p == 0.0 and q.dtype == torch.bfloat16
             and k.dtype == torch.bfloat16 and v.dtype == torch.bfloat16 and q.shape[-1] == 128
             and k.shape[-1] == 128 and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1
-            and q.shape[1] % k.shape[1] == 0 and all(s % 8 == 0 for t in (q, k, v) for s in t.stride()[:3]))
+            and q.shape[1] % k.shape[1] == 0 and all(s % 8 == 0 for t in (q, k, v) for s in t.stride()[:3])
+            and (not any(t.requires_grad for t in (q, k, v)) or q.shape[2] == k.shape[2]))
 
 
 def attention(q, k, v, causal=True, softmax_scale=None, attn_mask=None, dropout_p=0.0):

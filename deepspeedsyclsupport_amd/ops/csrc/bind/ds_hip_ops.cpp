@@ -48,6 +48,10 @@ int ds_flash_fwd(const void*, const void*, const void*, void*, float*, int, int,
 int ds_flash_fwd_sparse(const void*, const void*, const void*, void*, float*, int, int, int, int, const int64_t*,
                         const int64_t*, const int64_t*, const int64_t*, float, const int*, const int*, const int*,
                         const uint8_t*, int, int, int, int, hipStream_t);
+int ds_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, float*, void*,
+                 void*, void*, int, int, int, int, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
+                 const int64_t*, const int64_t*, const int64_t*, const int64_t*, float, int, const int*, const int*,
+                 const uint8_t*, int, int, int, int, hipStream_t);
 int ds_xent_fwd(const void*, const int64_t*, float*, float*, int64_t, int, int64_t, int, float, int, hipStream_t);
 int ds_xent_bwd(const void*, const int64_t*, const float*, const float*, float, void*, int64_t, int, int64_t, int64_t,
                 int, float, int, hipStream_t);
@@ -488,6 +492,63 @@ std::vector<Tensor> flash_fwd_sparse(Tensor q, Tensor k, Tensor v, double scale,
   return {o, lse};
 }
 
+// Flash backward (csrc/attn/flash_bwd.hip): q/o/dout [B,Hq,S,128], k/v [B,Hk,S,128] bf16 views with unit last stride,
+// lse [B,Hq,S] fp32 from flash_fwd. mode 0 full, 1 causal, 2 block-sparse with the column LUT (qtiles int32
+// [Hk, nkb, T] of (head-in-group << 16 | 32-row tile), nqt int32 [Hk, nkb], layout uint8 [LH, nb, nb], granularity
+// blk). Returns dq, dk, dv laid out [B,S,H,128] in memory (viewed [B,H,S,128]) like flash_fwd's output.
+std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dout, double scale,
+                              int64_t mode, OptT qtiles, OptT nqt, OptT layout, int64_t blk) {
+  for (const Tensor* t : {&q, &k, &v, &o, &dout}) {
+    TORCH_CHECK(t->is_cuda() && t->dim() == 4 && t->scalar_type() == at::kBFloat16, "flash_bwd: 4-D bf16 device tensors");
+    TORCH_CHECK(t->size(3) == 128 && t->stride(3) == 1, "flash_bwd: head dim 128 with unit last stride");
+    for (int d = 0; d < 3; ++d) TORCH_CHECK(t->stride(d) % 8 == 0, "flash_bwd: strides must be multiples of 8");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "flash_bwd: 16-B aligned data required");
+  }
+  const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), Hk = k.size(1);
+  TORCH_CHECK(k.size(0) == B && k.size(2) == S && v.sizes() == k.sizes(), "flash_bwd: k/v shape (S == Skv required)");
+  TORCH_CHECK(o.sizes() == q.sizes() && dout.sizes() == q.sizes(), "flash_bwd: o/dout shape");
+  TORCH_CHECK(Hq % Hk == 0, "flash_bwd: Hq must be a multiple of Hk");
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * Hq * S,
+              "flash_bwd: lse [B,Hq,S] fp32 contiguous");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "flash_bwd: mode");
+  const int* qt = nullptr; const int* nq = nullptr; const uint8_t* lay = nullptr;
+  int maxt = 0, LH = 1, nb = 0;
+  if (mode == 2) {
+    TORCH_CHECK(qtiles.has_value() && nqt.has_value() && layout.has_value(), "flash_bwd: sparse LUT required");
+    need(*qtiles, "qtiles"); need(*nqt, "nqt"); need(*layout, "layout");
+    TORCH_CHECK(qtiles->scalar_type() == at::kInt && nqt->scalar_type() == at::kInt &&
+                    layout->scalar_type() == at::kByte, "flash_bwd: int32 qtiles/nqt, uint8 layout");
+    const int64_t nkb = (S + 255) / 256;
+    LH = (int)layout->size(0); nb = (int)layout->size(1);
+    TORCH_CHECK(layout->dim() == 3 && layout->size(2) == nb && nb * blk >= S && (LH == 1 || LH == Hq),
+                "flash_bwd: layout [LH, nb, nb]");
+    TORCH_CHECK(qtiles->dim() == 3 && qtiles->size(0) == Hk && qtiles->size(1) == nkb && nqt->numel() == Hk * nkb,
+                "flash_bwd: LUT shape");
+    maxt = (int)qtiles->size(2);
+    if (nqt->numel() > 0) TORCH_CHECK(nqt->max().item<int>() <= maxt && nqt->min().item<int>() >= 0, "flash_bwd: nqt");
+    if (qtiles->numel() > 0) {  // the kernel trusts the LUT for its Q / dO addresses
+      const int ntq = (int)((S + 31) / 32), rep = (int)(Hq / Hk);
+      auto codes = qtiles->masked_fill(qtiles->lt(0), 0);
+      TORCH_CHECK((codes.bitwise_and(0xffff)).max().item<int>() < ntq && torch::bitwise_right_shift(codes, 16).max().item<int>() < rep,
+                  "flash_bwd: LUT entries out of range");
+    }
+    qt = qtiles->data_ptr<int>(); nq = nqt->data_ptr<int>(); lay = layout->data_ptr<uint8_t>();
+  }
+  auto mk = [&](int64_t H) { return torch::empty({B, S, H, 128}, q.options()).transpose(1, 2); };
+  auto dq = mk(Hq), dk = mk(Hk), dv = mk(Hk);
+  auto delta = torch::empty({B * Hq * S}, q.options().dtype(at::kFloat));
+  auto dqacc = torch::empty({B * Hq * S * 128}, q.options().dtype(at::kFloat));
+  auto st3 = [](const Tensor& t, int64_t* s) { for (int d = 0; d < 3; ++d) s[d] = t.stride(d); };
+  int64_t qs[3], ks[3], vs[3], os[3], gs[3], dqs[3], dks[3], dvs[3];
+  st3(q, qs); st3(k, ks); st3(v, vs); st3(o, os); st3(dout, gs); st3(dq, dqs); st3(dk, dks); st3(dv, dvs);
+  check(ds_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                     delta.data_ptr<float>(), dqacc.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                     (int)B, (int)Hq, (int)Hk, (int)S, qs, ks, vs, os, gs, dqs, dks, dvs, (float)scale, (int)mode, qt,
+                     nq, lay, maxt, LH, nb, (int)blk, stream()),
+        "flash_bwd");
+  return {dq, dk, dv};
+}
+
 }  // namespace
 
 // other binding translation units of this extension
@@ -524,6 +585,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_inplace", &rope_inplace);
   m.def("flash_fwd", &flash_fwd);
   m.def("flash_fwd_sparse", &flash_fwd_sparse);
+  m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"),
+        py::arg("dout"), py::arg("scale"), py::arg("mode"), py::arg("qtiles") = py::none(), py::arg("nqt") = py::none(),
+        py::arg("layout") = py::none(), py::arg("blk") = 0);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
 }

@@ -41,6 +41,7 @@ EXTENSIONS = {
             "xent/xent_kernels.hip",
             "attn/decode_attn.hip",
             "attn/flash_fwd.hip",
+            "attn/flash_bwd.hip",
             "quant/quant_kernels.hip",
             "gemv/skinny_gemm.hip",
             "gemv/skinny_mfma.hip",

@@ -6,9 +6,10 @@ head) visits only the 64-key tiles its layout rows touch, listed in a LUT built 
 length), and masks inside a tile at the layout's block granularity. Work and K/V traffic therefore scale with the
 layout density. Head dims below 128 are zero-padded to 128 (zeros change neither QK^T nor the kept part of PV).
 
-Backward: the memory-efficient attention backward fed with our (O, LSE) and the layout as an additive -inf bias,
-the same interchange the dense training path uses (`ops/attention.py`). It is exact for the sparse forward; its
-work is dense in the sequence length.
+Backward: `csrc/attn/flash_bwd.hip` in its SPARSE instantiation (reference: the transposed DSD/SDD products of
+`matmul.py:605` and the sparse softmax backward `softmax.py:213`) — every workgroup (256 keys of one head) visits
+only the 32-row query tiles its key block meets in the layout (a column LUT built here) and masks at the layout's
+block granularity, recomputing P from the forward's LSE. No [L, L] tensor is ever built; work scales with density.
 """
 import torch
 
@@ -54,8 +55,47 @@ def build_lut(layout, blk, L, device):
     return lut
 
 
+_BWD_LUTS = {}
+
+
+def build_bwd_lut(layout, blk, L, H, device):
+    """Column LUT of the sparse backward: (qtiles int32 [H, nkb, T] = 32-row query tiles met by each 256-key block,
+    ascending, nqt int32 [H, nkb], layout uint8 [LH, nb, nb] at granularity blk' = min(blk, 128), blk')."""
+    key = _lut_key(layout, blk, L, device) + (H,)
+    hit = _BWD_LUTS.get(key)
+    if hit is not None:
+        return hit
+    lay = layout.to(torch.bool)
+    if lay.shape[0] > 1 and bool((lay == lay[:1]).all()):
+        lay = lay[:1]
+    if blk > 128:  # the kernel masks at <= 128-row granularity: refine the layout
+        f = blk // 128
+        lay = lay.repeat_interleave(f, 1).repeat_interleave(f, 2)
+        blk = 128
+    LH, nb, _ = lay.shape
+    g = 16
+    fine = lay.repeat_interleave(blk // g, 1).repeat_interleave(blk // g, 2)[:, :L // g, :L // g]
+    nkb = (L + 255) // 256
+    ntq = L // 32
+    fine = torch.nn.functional.pad(fine, (0, nkb * 16 - fine.shape[2]))
+    met = fine.reshape(LH, ntq, 2, nkb, 16).any(4).any(2)      # [LH, ntq, nkb]
+    met = met.permute(0, 2, 1).contiguous()                     # [LH, nkb, ntq]
+    nqt = met.sum(-1).to(torch.int32)
+    T = max(int(nqt.max()), 1)
+    order = torch.sort((~met).to(torch.int8), dim=-1, stable=True).indices[..., :T].to(torch.int32)
+    if LH == 1 and H > 1:
+        order, nqt = order.expand(H, nkb, T), nqt.expand(H, nkb)
+    out = (order.contiguous().to(device), nqt.contiguous().to(device), lay.to(torch.uint8).contiguous().to(device),
+           blk)
+    if len(_BWD_LUTS) > 64:
+        _BWD_LUTS.clear()
+    _BWD_LUTS[key] = out
+    return out
+
+
 def token_bias(layout, blk, L, H, dtype, device):
-    """Additive [1, H, L, L] bias: 0 where the layout allows, -inf elsewhere (backward of the sparse forward)."""
+    """Additive [1, H, L, L] bias: 0 where the layout allows, -inf elsewhere. Reference semantics for tests and
+    host fallbacks only — the kernels never build it."""
     lay = layout.to(torch.bool)
     tok = lay.repeat_interleave(blk, 1).repeat_interleave(blk, 2)[:, :L, :L].to(device)
     if tok.shape[0] == 1 and H > 1:
@@ -77,14 +117,11 @@ class BlockSparseAttnFn(torch.autograd.Function):
         need_grad = any(t.requires_grad for t in (q, k, v))
         o, lse = hip_ops().flash_fwd_sparse(qp, kp, vp, float(scale), tiles, ntiles, qorder, lay_u8, int(blk),
                                               need_grad)
+        o_full = o
         if D < 128:
-            # keep the [B, L, H, D] memory layout the kernel wrote: the efficient-attention backward reads O with
-            # that layout (a [B, H, L, D]-contiguous O gives wrong dK/dV and can fault — tools/probe_sparse_bwd.py)
-            o_bl = torch.empty((B, L, H, D), dtype=o.dtype, device=o.device).transpose(1, 2)
-            o_bl.copy_(o[..., :D])
-            o = o_bl
+            o = o[..., :D]
         if need_grad:
-            ctx.save_for_backward(q, k, v, o, lse)
+            ctx.save_for_backward(q, k, v, o_full, lse)
             ctx.layout, ctx.blk, ctx.scale = layout, blk, float(scale)
         return o
 
@@ -92,11 +129,15 @@ class BlockSparseAttnFn(torch.autograd.Function):
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
         B, H, L, D = q.shape
-        bias = token_bias(ctx.layout, ctx.blk, L, H, q.dtype, q.device).expand(B, H, L, L)
-        z = torch.zeros((), dtype=torch.int64, device=q.device)
-        do = do if do.stride(-1) == 1 else do.contiguous()
-        dq, dk, dv, _ = torch.ops.aten._scaled_dot_product_efficient_attention_backward(
-            do, q, k, v, bias, o, lse, z, z, 0.0, [True, True, True, False], False, scale=ctx.scale)
+        qtiles, nqt, lay_u8, blk = build_bwd_lut(ctx.layout, ctx.blk, L, H, q.device)
+        if D < 128:
+            pad = (0, 128 - D)
+            q, k, v, do = (torch.nn.functional.pad(t, pad) for t in (q, k, v, do))
+        elif do.stride(-1) != 1 or any(s % 8 for s in do.stride()[:3]):
+            do = do.contiguous()
+        dq, dk, dv = hip_ops().flash_bwd(q, k, v, o, lse, do, ctx.scale, 2, qtiles, nqt, lay_u8, blk)
+        if D < 128:
+            dq, dk, dv = dq[..., :D], dk[..., :D], dv[..., :D]
         return dq, dk, dv, None, None, None
 
 

@@ -44,3 +44,33 @@ def test_token_bias_and_native_gate():
     assert torch.equal(b[0] == 0, lay.bool().repeat_interleave(16, 1).repeat_interleave(16, 2))
     q = torch.randn(1, 2, 256, 64)
     assert not bs.native_ok(q, q, q, 16)  # host tensors never take the kernel path
+
+
+@pytest.mark.parametrize("cfg", [
+    FixedSparsityConfig(num_heads=4, block=16, num_local_blocks=4),
+    BigBirdSparsityConfig(num_heads=4, block=32),
+    VariableSparsityConfig(num_heads=4, block=32, different_layout_per_head=True),
+    BigBirdSparsityConfig(num_heads=2, block=256),
+], ids=["fixed16", "bigbird32", "variable_perhead", "bigbird256"])
+@pytest.mark.parametrize("L", [1024, 1280])
+def test_bwd_column_lut_matches_brute_force(cfg, L):
+    """Sparse backward LUT: for every (head, 256-key block) the listed 32-row query tiles are exactly the tiles with
+    at least one allowed (query, key) pair inside the key block."""
+    if L % cfg.block:
+        pytest.skip("layout block must divide L")
+    lay = cfg.make_layout(L)
+    H = lay.shape[0]
+    qtiles, nqt, lay_u8, blk = bs.build_bwd_lut(lay, cfg.block, L, H, "cpu")
+    assert blk == min(cfg.block, 128)
+    nkb = (L + 255) // 256
+    assert tuple(qtiles.shape[:2]) == (H, nkb) and tuple(nqt.shape) == (H, nkb)
+    tok = lay.bool().repeat_interleave(cfg.block, 1).repeat_interleave(cfg.block, 2)[:, :L, :L]
+    for h in range(H):
+        for kb in range(nkb):
+            cols = tok[h, :, kb * 256:(kb + 1) * 256].any(1)
+            need = cols.reshape(L // 32, 32).any(-1).nonzero().flatten().tolist()
+            got = qtiles[h, kb, :nqt[h, kb]].tolist()
+            assert got == need, (h, kb)
+    # the refined layout is equivalent to the original at token level
+    tok2 = lay_u8.bool().repeat_interleave(blk, 1).repeat_interleave(blk, 2)[:, :L, :L]
+    assert torch.equal(tok2.expand_as(tok) if tok2.shape[0] == 1 else tok2, tok)
