@@ -39,9 +39,12 @@ class TorchCheckpointEngine(CheckpointEngine):
         torch.save(state_dict, path)
 
     def load(self, path: str, map_location=None):
-        # checkpoints hold only tensors / containers / primitives (the loss scaler is saved as a dict), so they load
-        # with the non-executing loader
-        return torch.load(path, map_location=map_location, weights_only=True)
+        # our checkpoints hold only tensors / containers / primitives (the loss scaler is saved as a dict), so they
+        # load with the non-executing loader; reference-written files additionally pickle a few inert objects
+        # (LossScaler, fragment_address), matched to allow-listed stand-ins (checkpoint/zero_checkpoint.py)
+        from ...checkpoint.zero_checkpoint import _reference_pickle_stubs
+        with torch.serialization.safe_globals(_reference_pickle_stubs()):
+            return torch.load(path, map_location=map_location, weights_only=True)
 
 
 def _to_host(obj):

@@ -524,14 +524,60 @@ class DeepSpeedEngine(nn.Module):
         return os.path.join(checkpoints_path, str(tag), f"{prefix}{dp_rank}_mp_rank_{mp_rank:02d}{CK.OPTIM_FILE_SUFFIX}")
 
     def module_state_dict(self, destination=None, prefix="", keep_vars=False, exclude_frozen_parameters=False):
-        """Full module state dict; under ZeRO-3 (dp>1 or offloaded params) this gathers every group (16-bit)."""
-        from .zero.partition_parameters import GatheredParameters
-        if self.zero_optimization_partition_weights() and (self.dp_world_size > 1 or
-                                                           getattr(self.optimizer, "offload_param", False)):
-            with GatheredParameters(list(self.module.parameters())):
-                sd = {k: v.detach().clone() for k, v in self.module.state_dict().items()}
-            return sd
-        return self.module.state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)
+        """The module's state dict as it stands (reference `runtime/engine.py:2520`): under ZeRO-3 the partitioned
+        parameters are empty placeholders — their values live in the per-rank optimizer shards, which is what
+        `save_checkpoint` writes and `load_checkpoint` restores from. Use `save_16bit_model` (or
+        `consolidated_16bit_state_dict`) for a full 16-bit copy."""
+        sd = self.module.state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)
+        if exclude_frozen_parameters:
+            for n, p in self.module.named_parameters():
+                if not p.requires_grad and n in sd:
+                    del sd[n]
+        return sd
+
+    def _zero3_partitioned(self):
+        opt = self.optimizer
+        return self.zero_optimization_partition_weights() and opt is not None and \
+            any((not g.persistent) or g.partition for g in getattr(opt, "groups", []))
+
+    @torch.no_grad()
+    def consolidated_16bit_state_dict(self, exclude_frozen_parameters=False, rank0_only=True):
+        """Full 16-bit state dict gathered ONE flat group at a time (reference `runtime/engine.py:3477-3592`
+        `_zero3_consolidated_16bit_state_dict`): every rank joins each group's all-gather, the gathering rank copies
+        the group's parameters to host memory, and the device buffer is dropped before the next group — so no rank
+        ever holds more than one gathered group on its GPU. Returns the dict on rank 0 (every rank when
+        rank0_only=False), None elsewhere."""
+        if not self._zero3_partitioned():
+            sd = self.module_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
+            return OrderedDict((k, v.detach().cpu().clone()) for k, v in sd.items())
+        opt = self.optimizer
+        keep = (not rank0_only) or dist.get_rank() == 0
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        out = OrderedDict()
+        for g in opt.groups:
+            if g.persistent and g.full is not None:
+                full = g.full
+            else:
+                shard = g.shard if g.shard.device == opt.device else g.shard.to(opt.device, non_blocking=True)
+                full = torch.empty(g.padded, dtype=g.shard.dtype, device=opt.device)
+                if g.partition:
+                    dist.all_gather_into_tensor(full, shard.contiguous(), group=g.dp_group)
+                else:
+                    full.copy_(shard)
+            if keep:
+                for i, p in enumerate(g.params):
+                    n = names.get(id(p))
+                    if n is not None:
+                        out[n] = full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).cpu().clone()
+            del full
+        if keep:
+            for n, t in self.module.state_dict().items():  # buffers and parameters the optimizer does not own
+                if n not in out and not (exclude_frozen_parameters and n in names.values() and
+                                         not dict(self.module.named_parameters())[n].requires_grad):
+                    out[n] = t.detach().cpu().clone()
+            ordered = OrderedDict((k, out[k]) for k in self.module.state_dict().keys() if k in out)
+            return ordered
+        return None
 
     def _param_shapes(self):
         shapes = OrderedDict()
@@ -556,7 +602,58 @@ class DeepSpeedEngine(nn.Module):
                 raise ValueError(msg)
             logger.warning(msg)
 
+    def _moe_layers(self):
+        from ..moe.layer import MoE
+        return [(n, m) for n, m in self.module.named_modules() if isinstance(m, MoE)]
+
+    def _expert_ckpt_name(self, save_dir, tag, layer_id, expert_id):
+        mp_rank = 0 if self.mpu is None else self.mpu.get_model_parallel_rank()
+        return os.path.join(save_dir, str(tag), f"{CK.LAYER_FILE_PREFIX}{layer_id}_expert_{expert_id}_mp_rank_"
+                            f"{mp_rank:02d}{CK.MODEL_FILE_SUFFIX}")
+
+    def _save_moe_experts(self, save_dir, tag, module_sd):
+        """One file per (MoE layer, GLOBAL expert id) with that expert's tensors (reference `_save_moe_checkpoint`,
+        `runtime/engine.py:3151-3200`); written by expert-data-parallel rank 0 of each expert-parallel group. The
+        expert entries are removed from `module_sd` (the main file holds only non-expert state)."""
+        from ..checkpoint.zero_checkpoint import _EXPERT_RE
+        for layer_id, (mname, m) in enumerate(self._moe_layers()):
+            prefix = (mname + ".") if mname else ""
+            keys = [k for k in list(module_sd.keys()) if k.startswith(prefix) and _EXPERT_RE.match(k)]
+            per_expert = {}
+            ep_rank = groups._get_expert_parallel_rank(m.expert_group_name) if dist.is_initialized() else 0
+            edp_rank = groups._get_expert_data_parallel_rank(m.expert_group_name) if dist.is_initialized() else 0
+            for k in keys:
+                t = module_sd.pop(k)
+                mm = _EXPERT_RE.match(k)
+                gid = ep_rank * m.num_local_experts + int(mm.group(2))
+                per_expert.setdefault(gid, OrderedDict())[f"{mm.group(1)}{gid}{mm.group(3)}"] = t.detach().clone()
+            if edp_rank != 0:
+                continue
+            for gid, esd in per_expert.items():
+                if all(t.numel() > 0 for t in esd.values()):  # ZeRO-3 placeholders live in the optimizer shards
+                    self.checkpoint_engine.save(esd, self._expert_ckpt_name(save_dir, tag, layer_id, gid))
+
+    def _load_moe_experts(self, load_dir, tag, module_sd):
+        """Merge this rank's local experts from the per-expert files into `module_sd` (global -> local ids)."""
+        from ..checkpoint.zero_checkpoint import _EXPERT_RE
+        for layer_id, (mname, m) in enumerate(self._moe_layers()):
+            ep_rank = groups._get_expert_parallel_rank(m.expert_group_name) if dist.is_initialized() else 0
+            for local in range(m.num_local_experts):
+                gid = ep_rank * m.num_local_experts + local
+                path = self._expert_ckpt_name(load_dir, tag, layer_id, gid)
+                if not os.path.exists(path):
+                    continue
+                esd = self.checkpoint_engine.load(path, map_location="cpu")
+                for k, v in esd.items():
+                    mm = _EXPERT_RE.match(k)
+                    module_sd[f"{mm.group(1)}{local}{mm.group(3)}" if mm else k] = v
+
     def save_checkpoint(self, save_dir, tag=None, client_state={}, save_latest=True, exclude_frozen_parameters=False):
+        """Reference layout (`runtime/engine.py:3050-3130`): `mp_rank_XX_model_states.pt` (ZeRO-3:
+        `zero_pp_rank_{dp}_mp_rank_XX_model_states.pt` per rank, holding the partitioned placeholders), one
+        `{bf16_}zero_pp_rank_{dp}_mp_rank_XX_optim_states.pt` per rank holding ONLY that rank's fp32 / moment shard
+        plus the flat-layout descriptor, MoE expert files, `latest`, and `zero_to_fp32.py`. No rank gathers
+        parameters it does not own."""
         if tag is None:
             tag = f"global_step{self.global_steps}"
         tag = str(tag)
@@ -566,9 +663,14 @@ class DeepSpeedEngine(nn.Module):
         dist.barrier()
         os.makedirs(os.path.join(save_dir, tag), exist_ok=True)
         module_sd = self.module_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
+        if getattr(self, "has_moe_layers", False):
+            self._save_moe_experts(save_dir, tag, module_sd)
         zero = self.optimizer is not None
-        state = dict(module=module_sd if (self.save_non_zero_checkpoint or self.zero_optimization_stage() == 3)
-                     else None,
+        sampler = None
+        dl = getattr(self, "training_dataloader", None)
+        if dl is not None and hasattr(getattr(dl, "data_sampler", None), "state_dict"):
+            sampler = dl.data_sampler.state_dict()
+        state = dict(module=module_sd if self.save_non_zero_checkpoint else None,
                      buffer_names=[n for n, _ in self.module.named_buffers()],
                      optimizer=None,
                      param_shapes=self._param_shapes() if zero else None,
@@ -576,7 +678,7 @@ class DeepSpeedEngine(nn.Module):
                      shared_params=None,
                      frozen_param_fragments=None,
                      lr_scheduler=self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,
-                     data_sampler=None,
+                     data_sampler=sampler,
                      random_ltd=None,
                      sparse_tensor_module_names=list(self.sparse_tensor_module_names),
                      skipped_steps=self.skipped_steps,
@@ -584,6 +686,7 @@ class DeepSpeedEngine(nn.Module):
                      global_samples=self.global_samples,
                      dp_world_size=self.seq_dp_world_size,
                      mp_world_size=self.mp_world_size,
+                     num_experts=getattr(self, "num_experts", None),
                      ds_config=self._config.param_dict,
                      ds_version=_version())
         state.update(client_state)
@@ -611,6 +714,12 @@ class DeepSpeedEngine(nn.Module):
 
     def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
                         load_lr_scheduler_states=True, load_module_only=False, custom_load_fn=None):
+        """Reference `runtime/engine.py:2688-3020`. Optimizer state is restored positionally when this rank's saved
+        flat layout equals the live one; otherwise (different data-parallel size, bucket size, persistence threshold,
+        Twin-Flow ratio, or a reference-format checkpoint) every parameter's fp32 master AND Adam moments are
+        rebuilt from all ranks' shards and re-partitioned (`checkpoint/zero_checkpoint.py`) — moments are never
+        silently dropped."""
+        from ..checkpoint import zero_checkpoint as zc
         if tag is None:
             latest = os.path.join(load_dir, "latest")
             if not os.path.isfile(latest):
@@ -618,47 +727,77 @@ class DeepSpeedEngine(nn.Module):
                 return None, None
             with open(latest) as f:
                 tag = f.read().strip()
+        tag_dir = os.path.join(load_dir, str(tag))
         path = self._get_ckpt_name(load_dir, tag)
-        if not os.path.exists(path) and self.zero_optimization_partition_weights():
-            # elastic: fewer files than ranks, read rank 0's module file (holds the full 16-bit module)
-            path = os.path.join(load_dir, str(tag), f"{CK.ZERO_FILE_PREFIX}0_mp_rank_00{CK.MODEL_FILE_SUFFIX}")
+        if not os.path.exists(path):
+            # different topology: any model-states file carries the replicated metadata (and, outside ZeRO-3, the
+            # full module)
+            cands = sorted(f for f in os.listdir(tag_dir) if f.endswith(CK.MODEL_FILE_SUFFIX) and "expert_" not in f)
+            if not cands:
+                raise FileNotFoundError(f"no model-states file in {tag_dir}")
+            path = os.path.join(tag_dir, cands[0])
         ck = self.checkpoint_engine.load(path, map_location="cpu")
-        self._load_module_state(ck["module"], strict=load_module_strict)
+        module_sd = dict(ck.get("module") or {})
+        if getattr(self, "has_moe_layers", False):
+            self._load_moe_experts(load_dir, tag, module_sd)
+        self._load_module_state(module_sd, strict=load_module_strict and not self._zero3_partitioned())
         universal = bool(self._config.checkpoint_config.get("load_universal", False)) \
             if isinstance(self._config.checkpoint_config, dict) else \
             bool(getattr(self._config.checkpoint_config, "load_universal", False))
-        if universal and not load_module_only and self.optimizer is not None:
+        # under partitioned ZeRO-3 the weights themselves live in the optimizer shards
+        need_shards = self.optimizer is not None and (not load_module_only or self._zero3_partitioned())
+        if universal and need_shards:
             from ..checkpoint.ds_to_universal import load_universal_into
-            load_universal_into(self.optimizer, self.module, os.path.join(load_dir, str(tag)))
-        elif not load_module_only and self.optimizer is not None:
+            load_universal_into(self.optimizer, self.module, tag_dir)
+        elif need_shards:
+            with_states = load_optimizer_states and not load_module_only
             zpath = self._get_zero_ckpt_name(load_dir, tag)
+            osd = None
             if os.path.exists(zpath):
-                zsd = self.checkpoint_engine.load(zpath, map_location="cpu")
-                osd = zsd["optimizer_state_dict"]
-                same_topology = osd.get(CK.PARTITION_COUNT, 1) == self.optimizer.partition_count()
-                if same_topology:
-                    self.optimizer.load_state_dict(osd, load_optimizer_states=load_optimizer_states)
-                else:
-                    log_dist("DP world size changed since save: restoring fp32 masters from 16-bit weights "
-                             "(elastic load; optimizer moments reset)", ranks=[0])
-                    self.optimizer.refresh_from_module()
+                osd = self.checkpoint_engine.load(zpath, map_location="cpu")["optimizer_state_dict"]
+            if osd is not None and CK.FLAT_LAYOUT in osd and \
+                    zc.layouts_match(osd[CK.FLAT_LAYOUT], self.optimizer.layout()):
+                self.optimizer.load_state_dict(osd, load_optimizer_states=with_states)
+            elif zc.optim_files(tag_dir):
+                src = zc.open_source(tag_dir, 0 if self.mpu is None else self.mpu.get_model_parallel_rank())
+                log_dist(f"load_checkpoint: re-partitioning {type(src).__name__} ({len(src.files)} shard files) "
+                         f"onto dp={self.optimizer.partition_count()}", ranks=[0])
+                zc.restore_from_source(self.optimizer, self.module, src, load_optimizer_states=with_states)
+                ref_osd = osd if osd is not None else zc.load_file(src.files[0])[CK.OPTIMIZER_STATE_DICT]
+                self._load_scaler_state(ref_osd)
             else:
                 self.optimizer.refresh_from_module()
         if load_lr_scheduler_states and self.lr_scheduler is not None and ck.get("lr_scheduler") is not None:
             self.lr_scheduler.load_state_dict(ck["lr_scheduler"])
+        dl = getattr(self, "training_dataloader", None)
+        if ck.get("data_sampler") is not None and dl is not None and hasattr(getattr(dl, "data_sampler", None),
+                                                                             "load_state_dict"):
+            dl.data_sampler.load_state_dict(ck["data_sampler"])
         self.global_steps = ck.get("global_steps", 0)
         self.global_samples = ck.get("global_samples", self.global_steps * self.train_batch_size())
         self.skipped_steps = ck.get("skipped_steps", 0)
         client_state = {k: v for k, v in ck.items() if k not in _CKPT_KEYS}
-        return os.path.join(load_dir, str(tag)), client_state
+        return tag_dir, client_state
+
+    def _load_scaler_state(self, osd):
+        opt = self.optimizer
+        ls = osd.get(CK.LOSS_SCALER)
+        if isinstance(ls, dict):
+            opt.loss_scaler.load_state_dict(ls)
+        elif ls is not None and hasattr(ls, "cur_scale"):  # reference LossScaler object (stubbed on load)
+            opt.loss_scaler.cur_scale = float(getattr(ls, "cur_scale"))
+        opt.dynamic_loss_scale = osd.get("dynamic_loss_scale", opt.dynamic_loss_scale)
 
     @torch.no_grad()
     def _load_module_state(self, sd, strict=True):
         if self.zero_optimization_partition_weights() and self.optimizer is not None:
             own = dict(self.module.named_parameters())
             for n, v in sd.items():
-                if n in own:
-                    self.optimizer.set_full_fp32_param(own[n], v.to(self.device))
+                p = own.get(n)
+                # partitioned placeholders (numel 0) are restored from the optimizer shards instead
+                if p is not None and torch.is_tensor(v) and v.numel() == getattr(p, "ds_numel", p.numel()) and \
+                        v.numel() > 0:
+                    self.optimizer.set_full_fp32_param(p, v.to(self.device))
             bufs = dict(self.module.named_buffers())
             for n, v in sd.items():
                 if n in bufs:
@@ -669,7 +808,8 @@ class DeepSpeedEngine(nn.Module):
             self.optimizer.refresh_from_module()
 
     def save_16bit_model(self, save_dir, save_filename="pytorch_model.bin", exclude_frozen_parameters=False):
-        sd = self.module_state_dict()
+        """Consolidated 16-bit weights, streamed group by group to rank 0 (reference `runtime/engine.py:3477`)."""
+        sd = self.consolidated_16bit_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
         if dist.get_rank() == 0:
             os.makedirs(save_dir, exist_ok=True)
             torch.save(sd, os.path.join(save_dir, save_filename))
@@ -682,5 +822,6 @@ class DeepSpeedEngine(nn.Module):
 _CKPT_KEYS = {
     "module", "buffer_names", "optimizer", "param_shapes", "frozen_param_shapes", "shared_params",
     "frozen_param_fragments", "lr_scheduler", "data_sampler", "random_ltd", "sparse_tensor_module_names",
-    "skipped_steps", "global_steps", "global_samples", "dp_world_size", "mp_world_size", "ds_config", "ds_version"
+    "skipped_steps", "global_steps", "global_samples", "dp_world_size", "mp_world_size", "ds_config", "ds_version",
+    "num_experts"
 }

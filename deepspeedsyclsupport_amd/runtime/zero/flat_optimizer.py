@@ -996,15 +996,26 @@ class FlatZeroOptimizer:
         return full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).clone()
 
     def layout(self):
-        """Describe the flat layout (for checkpoints / zero_to_fp32): per group: param names, shapes, offsets, seg."""
+        """Describe the flat layout (for checkpoints / zero_to_fp32 / elastic reload): per group the param names,
+        shapes, offsets, segment geometry, the runs (segment slice -> optimizer-group master offset), and for MoE
+        expert groups the GLOBAL checkpoint name of every expert parameter (expert-parallel ranks hold different
+        experts under the same local names)."""
+        from ...checkpoint.zero_checkpoint import global_param_names
         names = {id(p): n for n, p in self.module.named_parameters()}
+        gnames = global_param_names(self.module)
         out = []
         for g in self.groups:
-            out.append(dict(seg=g.seg, dp=g.dp, persistent=g.persistent, partition=bool(g.partition),
-                            seg_lo=int(g.seg_lo), padded=int(g.padded),
-                            params=[(names.get(id(p), f"param_{id(p)}"), list(p.ds_shape), g.offsets[i], g.numels[i])
-                                    for i, p in enumerate(g.params)],
-                            runs=[(s, e, og, moff, on_host) for (s, e, og, moff, on_host) in g.runs]))
+            og0 = self.param_to_og[id(g.params[0])]
+            moe = self.optimizer.param_groups[og0].get("moe", False)
+            entry = dict(seg=g.seg, dp=g.dp, persistent=g.persistent, partition=bool(g.partition),
+                         seg_lo=int(g.seg_lo), padded=int(g.padded), rank=int(g.rank),
+                         params=[(names.get(id(p), f"param_{id(p)}"), list(p.ds_shape), g.offsets[i], g.numels[i])
+                                 for i, p in enumerate(g.params)],
+                         runs=[(s, e, og, moff, on_host) for (s, e, og, moff, on_host) in g.runs])
+            if moe:
+                entry["moe_group"] = self.optimizer.param_groups[og0].get("name")
+                entry["global_names"] = {n: gnames.get(n, n) for (n, _, _, _) in entry["params"]}
+            out.append(entry)
         return out
 
     # ================================================================================ checkpoint state

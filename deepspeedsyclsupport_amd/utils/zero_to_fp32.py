@@ -9,8 +9,13 @@ Each rank's `*_optim_states.pt` holds its fp32 master partitions (`single_partit
 tensor per optimizer group) plus a layout descriptor (`ds_flat_layout`): for every flat parameter group, the
 per-rank segment size / offset, which slices ("runs") of the segment live in which optimizer-group master at which
 offset (or in the host master for Twin-Flow / offload runs), and (name, shape, offset, numel) of every parameter.
-Reassembly = concatenate the ranks' segments per group, then slice parameters out. Files are read with
-`torch.load(weights_only=True)`.
+Reassembly is per parameter over every rank's own layout, so MoE expert groups (partitioned over expert-data-
+parallel ranks; expert-parallel ranks hold different experts, recorded under their global expert ids) and
+model-parallel ranks (one rank's files at a time) come out right. Files are read with `torch.load(weights_only=True)`.
+
+Format note: the flat-group shards are NOT the reference's per-group layout (`single_partition_of_fp32_groups`
+sliced by `param_shapes`), so the reference's zero_to_fp32 cannot read them; this script can, and
+`checkpoint/zero_checkpoint.py` reads both formats (the engine loads reference-format checkpoints through it).
 """
 import argparse
 import glob
@@ -33,19 +38,22 @@ def _load(path):
 
 
 def _rank_of(path):
-    m = re.search(r"zero_pp_rank_(\d+)_", os.path.basename(path))
-    return int(m.group(1)) if m else 0
+    m = re.search(r"zero_pp_rank_(\d+)_mp_rank_(\d+)", os.path.basename(path))
+    return (int(m.group(2)), int(m.group(1))) if m else (0, 0)
 
 
-def get_optim_files(ckpt_dir):
-    files = sorted(glob.glob(os.path.join(ckpt_dir, f"*{OPTIM_FILE_SUFFIX}")), key=_rank_of)
+def get_optim_files(ckpt_dir, mp_rank=0):
+    files = sorted((f for f in glob.glob(os.path.join(ckpt_dir, f"*{OPTIM_FILE_SUFFIX}")) if "zero_pp_rank_" in f),
+                   key=_rank_of)
+    if any(_rank_of(f)[0] == mp_rank for f in files):
+        files = [f for f in files if _rank_of(f)[0] == mp_rank]  # one model-parallel rank's data-parallel shards
     if not files:
         raise FileNotFoundError(f"no *{OPTIM_FILE_SUFFIX} files in {ckpt_dir}")
     return files
 
 
 def get_model_state_file(ckpt_dir):
-    files = sorted(glob.glob(os.path.join(ckpt_dir, f"*{MODEL_FILE_SUFFIX}")))
+    files = sorted(f for f in glob.glob(os.path.join(ckpt_dir, f"*{MODEL_FILE_SUFFIX}")) if "expert_" not in f)
     if not files:
         raise FileNotFoundError(f"no *{MODEL_FILE_SUFFIX} files in {ckpt_dir}")
     return files[0]
@@ -85,21 +93,36 @@ def _flat_source(st, key):
 
 
 def _reassemble(states, key):
-    layout0 = states[0][FLAT_LAYOUT]
+    """Per-parameter reassembly from EVERY rank's own layout (groups may differ per rank: MoE expert groups are
+    partitioned over expert-data-parallel ranks and expert-parallel ranks hold different experts, so expert parameters
+    are keyed by their GLOBAL name). Raises when the ranks' shards do not cover a parameter completely."""
+    index = OrderedDict()
+    for r, st in enumerate(states):
+        for g in st[FLAT_LAYOUT]:
+            gn = g.get("global_names") or {}
+            for (name, shape, off, numel) in g["params"]:
+                index.setdefault(gn.get(name, name), []).append((r, g, tuple(shape), off, numel))
     out = OrderedDict()
-    for gi, g in enumerate(layout0):
-        full = torch.zeros(g["padded"], dtype=torch.float32)
-        owners = range(len(states)) if g["partition"] else [0]
-        for r in owners:
-            st = states[r]
-            lg = st[FLAT_LAYOUT][gi]
-            fetch = _flat_source(st, key)
-            for (s, e, og, moff, on_host) in lg["runs"]:
+    for name, ents in index.items():
+        shape, numel = ents[0][2], ents[0][4]
+        buf = torch.zeros(numel, dtype=torch.float32)
+        cov = torch.zeros(numel, dtype=torch.bool)
+        for (r, g, _, off, _) in ents:
+            fetch = _flat_source(states[r], key)
+            lo = g["seg_lo"]
+            for (s, e, og, moff, on_host) in g["runs"]:
+                a, b = max(lo + s, off), min(lo + e, off + numel)
+                if a >= b:
+                    continue
                 src = fetch(og, on_host)
-                if src is not None:
-                    full[lg["seg_lo"] + s:lg["seg_lo"] + e] = src[moff:moff + e - s].float()
-        for name, shape, off, numel in g["params"]:
-            out[name] = full[off:off + numel].view(shape).clone()
+                if src is None:
+                    continue
+                buf[a - off:b - off] = src[moff + a - lo - s:moff + b - lo - s].float()
+                cov[a - off:b - off] = True
+        if not bool(cov.all()):
+            raise ValueError(f"'{name}': the {len(states)} shard files cover {int(cov.sum())}/{numel} elements "
+                             f"(missing rank files?)")
+        out[name] = buf.view(shape)
     return out
 
 
@@ -110,11 +133,14 @@ def load_optim_states(ds_checkpoint_dir):
 def _get_fp32_state_dict_from_zero_checkpoint(ds_checkpoint_dir, exclude_frozen_parameters=False):
     states = load_optim_states(ds_checkpoint_dir)
     out = _reassemble(states, "fp32")
+    # non-expert parameters whose 16-bit placeholders are empty (ZeRO-3) come only from the shards above
     # buffers (and any non-partitioned tensors) come from the 16-bit model file
     try:
         model_sd = _load(get_model_state_file(ds_checkpoint_dir))
         buffers = set(model_sd.get(BUFFER_NAMES, []) or [])
         for k, v in (model_sd.get("module") or {}).items():
+            if torch.is_tensor(v) and v.numel() == 0:
+                continue  # partitioned placeholder
             if k in buffers or (k not in out and not exclude_frozen_parameters):
                 out[k] = v.float() if torch.is_floating_point(v) else v
     except FileNotFoundError:

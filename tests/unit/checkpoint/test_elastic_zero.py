@@ -1,0 +1,177 @@
+"""ZeRO checkpoints across data-parallel sizes (reference `tests/unit/checkpoint/test_zero_optimizer.py:179-216`
+elastic save-at-N / load-at-M via DistributedFixture, `test_reshape_checkpoint.py`):
+
+* save at world 4 (ZeRO-2 and ZeRO-3, with a small reduce bucket / persistence threshold so every rank owns real
+  partitions), load at world 2 and 1: every fp32 master AND both Adam moments come back bit-exact (they are
+  re-partitioned, never reset), the step count is restored, and the next training step on the same global batch
+  gives the same loss at every world size;
+* ZeRO-3 save writes only per-rank shards: model files hold empty placeholders for partitioned parameters, and the
+  16-bit consolidation is streamed one group at a time (peak gathered bytes per rank = the largest group);
+* the DS_ZERO_FORCE_PARTITION single-rank rehearsal round-trips (its released parameters are restored from the
+  shards, not from zero-element module tensors).
+"""
+import os
+
+import pytest
+import torch
+
+from ..common import run_distributed
+from ..simple_model import base_config, random_tokens, tiny_llama
+
+GLOBAL = 4   # sequences per global batch
+SEQ = 16
+
+
+def _cfg(stage, world):
+    c = base_config(stage=stage, lr=1e-2, mb=GLOBAL // world, dtype="fp32")
+    c["train_batch_size"] = GLOBAL
+    c["zero_optimization"].update({"reduce_bucket_size": 3000, "stage3_param_persistence_threshold": 100,
+                                   "allgather_bucket_size": 3000})
+    return c
+
+
+def _slice(batch, world, rank):
+    per = GLOBAL // world
+    return batch[rank * per:(rank + 1) * per]
+
+
+def _step(eng, batch, world, rank):
+    x = _slice(batch, world, rank)
+    loss = eng(x, labels=x)
+    eng.backward(loss)
+    eng.step()
+
+
+def _eval_loss(eng, batch):
+    from deepspeedsyclsupport_amd import comm as dist
+    with torch.no_grad():
+        loss = eng(batch, labels=batch)
+    t = torch.tensor([float(loss)])
+    dist.all_reduce(t)  # every rank evaluates the same batch; average to be placement independent
+    return float(t) / dist.get_world_size()
+
+
+def _full_state(eng):
+    from deepspeedsyclsupport_amd.utils import safe_get_full_fp32_param, safe_get_full_optimizer_state
+    return {n: (safe_get_full_fp32_param(p), safe_get_full_optimizer_state(p, "exp_avg"),
+                safe_get_full_optimizer_state(p, "exp_avg_sq")) for n, p in eng.module.named_parameters()}
+
+
+def _save_at(stage, ckpt, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    data = random_tokens(4, GLOBAL, SEQ, seed=11)
+    eng, _, _, _ = ds.initialize(model=tiny_llama(), config=_cfg(stage, world))
+    assert eng.optimizer.partition_count() == world
+    for s in range(2):
+        _step(eng, data[s], world, rank)
+    eng.save_checkpoint(ckpt, tag="e")
+    saved = _full_state(eng)
+    _step(eng, data[2], world, rank)
+    cont = _eval_loss(eng, data[3])
+    if rank == 0:
+        torch.save({"state": saved, "cont": cont, "steps": eng.global_steps - 1}, out)
+
+
+def _load_at(stage, ckpt, ref_path, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    data = random_tokens(4, GLOBAL, SEQ, seed=11)
+    ref = torch.load(ref_path, weights_only=True)
+    eng, _, _, _ = ds.initialize(model=tiny_llama(seed=5), config=_cfg(stage, world))
+    eng.load_checkpoint(ckpt, tag="e")
+    assert eng.global_steps == ref["steps"]
+    got = _full_state(eng)
+    for n, (w, m, v) in ref["state"].items():
+        torch.testing.assert_close(got[n][0], w, rtol=0, atol=0, msg=f"{n} fp32")
+        torch.testing.assert_close(got[n][1], m, rtol=0, atol=0, msg=f"{n} exp_avg")
+        torch.testing.assert_close(got[n][2], v, rtol=0, atol=0, msg=f"{n} exp_avg_sq")
+    _step(eng, data[2], world, rank)
+    cont = _eval_loss(eng, data[3])
+    if rank == 0:
+        torch.save({"cont": cont}, out)
+
+
+@pytest.mark.parametrize("stage", [2, 3])
+def test_save_world4_load_world2_and_1(stage, tmp_path):
+    ckpt, ref = str(tmp_path / "ck"), str(tmp_path / "ref.pt")
+    run_distributed(_save_at, 4, stage, ckpt, ref)
+    # ZeRO-3: the module files carry placeholders only, shards carry the values
+    files = sorted(os.listdir(os.path.join(ckpt, "e")))
+    assert sum(f.endswith("_optim_states.pt") for f in files) == 4
+    if stage == 3:
+        ms = torch.load(os.path.join(ckpt, "e", "zero_pp_rank_1_mp_rank_00_model_states.pt"), weights_only=True)
+        assert any(v.numel() == 0 for v in ms["module"].values())
+    r = torch.load(ref, weights_only=True)
+    for world in (2, 1):
+        out = str(tmp_path / f"w{world}.pt")
+        run_distributed(_load_at, world, stage, ckpt, ref, out)
+        got = torch.load(out, weights_only=True)
+        assert got["cont"] == pytest.approx(r["cont"], rel=1e-5, abs=1e-6), world
+
+
+def _consolidate(ckpt_dir, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.utils import safe_get_full_fp32_param
+    world, rank = dist.get_world_size(), dist.get_rank()
+    eng, _, _, _ = ds.initialize(model=tiny_llama(), config=_cfg(3, world))
+    _step(eng, random_tokens(1, GLOBAL, SEQ, seed=3)[0], world, rank)
+    opt = eng.optimizer
+    # track the largest gathered buffer allocated during consolidation
+    biggest = {"n": 0}
+    real_empty = torch.empty
+
+    def spy(*a, **k):
+        t = real_empty(*a, **k)
+        biggest["n"] = max(biggest["n"], t.numel())
+        return t
+    torch.empty = spy
+    try:
+        sd = eng.consolidated_16bit_state_dict()
+    finally:
+        torch.empty = real_empty
+    largest_group = max(g.padded for g in opt.groups)
+    assert biggest["n"] <= largest_group, (biggest["n"], largest_group)
+    ref = {n: safe_get_full_fp32_param(p) for n, p in eng.module.named_parameters()}
+    eng.save_16bit_model(ckpt_dir)
+    if rank == 0:
+        assert set(sd) >= set(ref)
+        for n, v in ref.items():
+            torch.testing.assert_close(sd[n].float(), v, rtol=0, atol=0)
+        torch.save(ref, out)
+    else:
+        assert sd is None
+
+
+def test_zero3_consolidation_streams_groups(tmp_path):
+    out = str(tmp_path / "ref.pt")
+    run_distributed(_consolidate, 2, str(tmp_path / "m"), out)
+    sd = torch.load(str(tmp_path / "m" / "pytorch_model.bin"), weights_only=True)
+    ref = torch.load(out, weights_only=True)
+    for n, v in ref.items():
+        torch.testing.assert_close(sd[n].float(), v)
+
+
+def _forced_roundtrip(ckpt):
+    import deepspeedsyclsupport_amd as ds
+    os.environ["DS_ZERO_FORCE_PARTITION"] = "1"  # in the worker: a forkserver started earlier keeps its env
+    eng, _, _, _ = ds.initialize(model=tiny_llama(), config=_cfg(3, 1))
+    assert any(not g.persistent for g in eng.optimizer.groups), "forced partition must release groups"
+    data = random_tokens(3, GLOBAL, SEQ, seed=9)
+    _step(eng, data[0], 1, 0)
+    ref = _full_state(eng)
+    eng.save_checkpoint(ckpt, tag="f")
+    eng2, _, _, _ = ds.initialize(model=tiny_llama(seed=3), config=_cfg(3, 1))
+    eng2.load_checkpoint(ckpt, tag="f")
+    got = _full_state(eng2)
+    for n, (w, m, v) in ref.items():
+        torch.testing.assert_close(got[n][0], w, rtol=0, atol=0)
+        torch.testing.assert_close(got[n][1], m, rtol=0, atol=0)
+    _step(eng2, data[1], 1, 0)
+
+
+def test_forced_partition_roundtrip(tmp_path):
+    run_distributed(_forced_roundtrip, 1, str(tmp_path / "f"))
