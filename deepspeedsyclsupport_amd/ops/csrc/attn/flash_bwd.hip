@@ -12,34 +12,41 @@
 //  * "key on the lane": S = Q.K^T and dP = dO.V^T put the key on the MFMA column, so their accumulators are already
 //    the B operands of dV^T += dO^T.P and dK^T += Q^T.dS (accumulator-as-operand, no LDS round trip); the query-side
 //    A operands of those two products come from the same LDS image of the Q / dO tile through the hardware transposed
-//    read `ds_read_b64_tr_b16`; the image is XOR-swizzled so row reads (S, dP) and transposed reads are conflict-free;
-//  * dP's accumulator starts at -delta (delta = rowsum(dO*O), one preprocessing pass), so dS = P*(dP-delta) is one
-//    multiply; P = exp2(S*c - LSE*log2e) needs no row max;
+//    read `ds_read_b64_tr_b16`; the image is XOR-swizzled so row reads (S, dP) and transposed reads are conflict-free
+//    (SQ_LDS_BANK_CONFLICT = 0 measured);
+//  * S's accumulator starts at -LSE/scale and dP's at -delta (delta = rowsum(dO*O), one preprocessing pass), so
+//    P = exp2(c*S') needs no row max and dS = P*dP' is one multiply;
 //  * dS crosses LDS once (dS^T image, 64-B rows, 8-B units swizzled by key so the packed stores of 8 rows and the
 //    transposed reads are both conflict-free); waves 0..3 then compute the 32x128 dQ tile over all 256 keys
 //    (A = dS by transposed read, B = K by transposed read of the resident K image) and add it with packed-row f32
 //    atomics (one 32x32 accumulator register = two 128-B row segments = the full-rate atomic shape); waves 4..7 run
 //    ahead into the next tile, so the two waves on a SIMD keep its matrix core busy across the dQ phase;
-//  * one barrier per tile: the next Q / dO tile is fetched into registers before the current tile's MFMAs and written
-//    to the other LDS buffer after them (double-buffered Q/dO and dS images);
+//  * Q / dO / lse / delta tiles arrive by LDS-DMA (global_load_lds, issued from inline asm so hipcc does not drain it)
+//    two tiles ahead into a 3-deep ring, with the swizzle applied on the source address; one raw barrier per tile
+//    behind a counted `s_waitcnt vmcnt(N)`;
+//  * every LDS address is a per-lane base + an XOR toggle + a compile-time displacement; the bases are laundered per
+//    tile so hipcc does not hoist ~40 derived addresses into registers (2 waves per SIMD leave 256 per lane);
 //  * causal: waves whose 32 keys lie entirely above a tile skip it, the dQ product stops at the diagonal, workgroups
 //    with the most tiles (low key blocks) start first, and each (batch, kv head)'s key blocks share an XCD (Q / dO
 //    reuse in L2);
 //  * block-sparse: each workgroup walks only the 32-row query tiles its key block meets in the layout (a host-built
 //    column LUT) and masks at the layout's block granularity (16/32/64/128) — cost scales with the layout density.
+// Measured (tools/bench_flash_bwd.py, profiles/flash_bwd_bench_r2.jsonl): B8 H32 S4096 D128 causal 4.5 ms.
 #include "ds_hip.h"
+
+#include <cstdlib>
 
 namespace {
 
 constexpr int D = 128;
-constexpr int NW = 8;                  // waves per workgroup
-constexpr int NTHR = NW * 64;
-constexpr int KB = 32 * NW;            // keys per workgroup
+constexpr int KB = 256;                // keys per workgroup
 constexpr int QT = 32;                 // query rows per tile
 constexpr int TILE = QT * D * 2;       // 8 KB: one Q or dO tile
 constexpr int K_BYTES = KB * 256;      // resident K image
 constexpr int DS_BYTES = KB * 64;      // dS^T image [KB keys][32 q] bf16
-constexpr int LDS_BYTES = K_BYTES + 4 * TILE + 2 * DS_BYTES + 2 * 64 * 4 + 2 * NW;
+constexpr int NBUF = 3;                // Q / dO / lse / delta tiles in flight: two ahead of the one in use
+template <int NW>
+constexpr int lds_bytes() { return K_BYTES + NBUF * 2 * TILE + 2 * DS_BYTES + NBUF * 64 * 4 + 2 * 8; }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
@@ -47,6 +54,34 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glob_void;
+
+// LDS-DMA: every lane fetches `size` bytes from its own global address; they land at lds_base + lane * size.
+// Issued from inline asm on purpose: hipcc tracks its own global_load_lds builtins and then waits vmcnt(0) before
+// every LDS read it cannot prove disjoint from the DMA target (i.e. all of them, one LDS array) and before every use
+// of an older ordinary load, draining the prefetch. Out of its sight the DMA is ordered only by the counted
+// `s_waitcnt vmcnt(N)` + barrier below (in-order vmcnt: the compiler's own counts stay conservative).
+__device__ __forceinline__ void glds16(const void* g, const char* lds_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds_base);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
+}
+__device__ __forceinline__ void glds4(const void* g, const char* lds_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds_base);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
+}
 
 // 256-B rows of 16 x 16-B chunks, chunk XOR-swizzled by row mod 16 (same image as flash_fwd.hip): conflict-free for
 // 32-row b128 reads of one chunk and for 4-row transposed reads.
@@ -85,12 +120,20 @@ struct BwdArgs {
   const int* nqt;
   const uint8_t* layout;
   int maxt, lay_heads, nb, blk;
+  int dbg;  // experiment switches (DS_FLASH_BWD_DBG): 1 no atomics, 2 no dQ phase, 4 no dK/dV products, 8 no S/dP
 };
 
-template <bool CAUSAL, bool SPARSE>
-__global__ void __launch_bounds__(NTHR, 1) flash_bwd_kernel(BwdArgs a) {
+// NW waves per workgroup, each owning KPW = 256 / NW keys (NC = KPW / 32 column tiles of the S / dP accumulators).
+// NW = 4: one wave per SIMD with the whole 512-register file (dK^T/dV^T of 64 keys = 256 accumulator registers),
+// every wave also computes one 32-column slice of the tile's dQ; NW = 8: two waves per SIMD, 32 keys each, waves
+// 0..3 compute dQ.
+template <int NW, bool CAUSAL, bool SPARSE>
+__global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
+  constexpr int NTHR = NW * 64, KPW = KB / NW, NC = KPW / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  // the wave index lives in a scalar register (wave-uniform), everything lane-dependent in vector registers
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+            l32 = lane & 31;
   const int S = a.S;
   const int nkb = (S + KB - 1) / KB;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -100,10 +143,10 @@ __global__ void __launch_bounds__(NTHR, 1) flash_bwd_kernel(BwdArgs a) {
   const int ntq = (S + QT - 1) / QT;
 
   char* Kimg = smem;
-  char* QD = smem + K_BYTES;               // [buf][Q tile | dO tile]
-  char* DSimg = QD + 4 * TILE;             // [buf][KB][32] bf16
-  float* LD = reinterpret_cast<float*>(DSimg + 2 * DS_BYTES);  // [buf][lse/scale (32) | delta (32)]
-  uint8_t* FL = reinterpret_cast<uint8_t*>(LD + 2 * 64);            // [buf][wave]: slab met the tile
+  char* QD = smem + K_BYTES;                      // [NBUF][Q tile | dO tile]
+  char* DSimg = QD + NBUF * 2 * TILE;             // [2][KB][32] bf16
+  float* LD = reinterpret_cast<float*>(DSimg + 2 * DS_BYTES);  // [NBUF][lse (32) | delta (32)]
+  uint8_t* FL = reinterpret_cast<uint8_t*>(LD + NBUF * 64);       // [2][8 slabs]: slab met the tile
 
   const bf16* Kp = a.k + b * a.ksb + hk * a.ksh;
   const bf16* Vp = a.v + b * a.vsb + hk * a.vsh;
@@ -130,104 +173,169 @@ __global__ void __launch_bounds__(NTHR, 1) flash_bwd_kernel(BwdArgs a) {
   };
 
   // ------------------------------------------------------------------ staging of one (Q, dO, lse, delta) tile
-  // thread t moves 16-B chunk t of the Q tile and of the dO tile (32 rows x 16 chunks = 512 each)
-  u32x4_t qreg, oreg;
-  float lreg = 0.f;
-  const float inv_scale = 1.f / a.scale;
-  const int srow = tid >> 4, sch = tid & 15;
-  auto stage_load = [&](int it) {
+  // by LDS-DMA, two tiles ahead of the one being computed (no staging registers, no wait until the barrier that
+  // precedes its use). Wave w fills the 1-KB pieces w (and w+8 when NW = 4) of the swizzled Q and dO images: lane L
+  // of piece j lands at physical chunk 64j + L, i.e. row 4j + L/16, physical chunk L%16, so it fetches the logical
+  // chunk (L%16) ^ swizzle(row) — the swizzle goes on the SOURCE address. Wave 0 also moves the 32 lse and 32 delta
+  // values (4 B per lane). Per tile a wave issues dma_ops() vector-memory instructions.
+  constexpr int PIECES = 8 / NW;  // 1-KB pieces of one 8-KB tile per wave
+  auto stage = [&](int it, int buf) {
     int hq, qt;
     tile_at(it, hq, qt);
-    const int qrow = qt * QT + srow;
-    const int qr = min(qrow, S - 1);
-    qreg = *reinterpret_cast<const u32x4_t*>(a.q + b * a.qsb + hq * a.qsh + (int64_t)qr * a.qss + sch * 8);
-    oreg = *reinterpret_cast<const u32x4_t*>(a.dout + b * a.osb + hq * a.osh + (int64_t)qr * a.oss + sch * 8);
-    if (tid < 64) {
-      const int r = qt * QT + (tid & 31);
-      const int64_t idx = ((int64_t)b * a.Hq + hq) * S + min(r, S - 1);
-      if (tid < 32)
-        lreg = r < S ? a.lse[idx] * inv_scale : INFINITY;  // S starts at -LSE/scale; p = 0 on padded rows
-      else
-        lreg = r < S ? a.delta[idx] : 0.f;
+    int lane = threadIdx.x & 63;  // re-derived (and laundered) here: hoisted lane values were spilled
+    asm volatile("" : "+v"(lane));
+    const bf16* qb = a.q + b * a.qsb + hq * a.qsh;
+    const bf16* ob = a.dout + b * a.osb + hq * a.osh;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int j = w + i * NW, row = 4 * j + (lane >> 4), pch = lane & 15;
+      const int ch = pch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+      const int64_t qr = min(qt * QT + row, S - 1);
+      glds16(qb + qr * a.qss + ch * 8, QD + buf * 2 * TILE + 1024 * j);
+      glds16(ob + qr * a.oss + ch * 8, QD + buf * 2 * TILE + TILE + 1024 * j);
+    }
+    if (w == 0) {
+      const int r = min(qt * QT + (lane & 31), S - 1);
+      const int64_t idx = ((int64_t)b * a.Hq + hq) * S + r;
+      glds4(lane < 32 ? (const void*)(a.lse + idx) : (const void*)(a.delta + idx), (const char*)(LD + buf * 64));
     }
   };
-  auto stage_store = [&](int buf) {
-    *reinterpret_cast<u32x4_t*>(QD + buf * 2 * TILE + lds_off(srow, sch)) = qreg;
-    *reinterpret_cast<u32x4_t*>(QD + buf * 2 * TILE + TILE + lds_off(srow, sch)) = oreg;
-    if (tid < 64) LD[buf * 64 + tid] = lreg;
+  // s_waitcnt vmcnt(N) with N = the DMA instructions this wave issued for the newest tile (so the older tile has
+  // landed), then lgkmcnt(0) (this wave's LDS writes done) and the raw barrier (no vmcnt(0) drain)
+  auto barrier_keep_newest = [&](bool newest_in_flight) {
+    if (newest_in_flight) {
+      if (w == 0) {
+        if (PIECES == 1) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        if (PIECES == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
   };
+  const float inv_scale = 1.f / a.scale;
 
-  // ------------------------------------------------------------------ resident K image + per-wave K / V fragments
+  // ------------------------------------------------------------------ resident K image + per-wave V fragments
   for (int i = tid; i < KB * 16; i += NTHR) {
     const int row = i >> 4, ch = i & 15;
     const int key = min(k0 + row, S - 1);
     *reinterpret_cast<u32x4_t*>(Kimg + lds_off(row, ch)) =
         *reinterpret_cast<const u32x4_t*>(Kp + (int64_t)key * a.kss + ch * 8);
   }
-  const int kw0 = k0 + 32 * w;        // first key of this wave
-  const int mykey = kw0 + l32;        // this lane's key (column of S / dP)
+  const int kw0 = k0 + KPW * w;       // first key of this wave
   // V rows stay in registers (B operand of dP); K rows are read from the resident image (it also feeds dQ)
-  bf16x8_t vf[8];
-  {
-    const int kr = min(mykey, S - 1);
+  bf16x8_t vf[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int kr = min(kw0 + 32 * c + l32, S - 1);
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk)
-      vf[kk] = *reinterpret_cast<const bf16x8_t*>(Vp + (int64_t)kr * a.vss + 16 * kk + 8 * h);
+      vf[c][kk] = *reinterpret_cast<const bf16x8_t*>(Vp + (int64_t)kr * a.vss + 16 * kk + 8 * h);
   }
 
-  f32x16_t dk[4], dv[4];
+  // ------------------------------------------------------------------ per-lane LDS address bases
+  // transposed-read lane geometry (see flash_fwd.hip): lane reads row rb + gq, 16-B chunk c0 + 2*colhalf + gch,
+  // byte gb; it receives rows rb..rb+3 of column (lane & 31) of the addressed 32-column slab. Displacements of 16
+  // rows keep the swizzle phase, so every address is  base + (small XOR term) + compile-time displacement: the
+  // XOR of the chunk index with the row's swizzle splits into a per-lane base and a 2-3-bit per-lane toggle.
+  // The bases are laundered at the top of each tile (asm) so hipcc recomputes the few derived addresses (2 VALU
+  // each) instead of hoisting ~40 of them into registers — at 2 waves per SIMD that is the difference between
+  // spilling and not.
+  const int gq = (lane >> 2) & 3, gch = (lane >> 1) & 1, gb = 8 * (lane & 1), colhalf = (lane >> 4) & 1;
+  const int ds_unit = 4 * colhalf + 2 * gch + (lane & 1);
+  auto swz = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
+  // row reads: lds_off(l32, 2kk+h) = rbase + 32 * (kk ^ rtog)
+  int rbase = l32 * 256 + 16 * ((h ^ swz(l32)) & 1), rtog = swz(l32) >> 1;
+  // transposed tile reads: lds_off(4h+8hi+gq, 4dt + 2colhalf + gch) + gb = tbase[hi] + 64 * (dt ^ ttog[hi])
+  int tbase[2], ttog[2];
+  // dQ: transposed reads of the K image and of the dS^T image (no toggle: 16-row steps)
+  const int wq = w & 3;  // the 32-column d slice of dQ this wave computes (waves 0..3)
+  int kqoff[2], dsqoff[2];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dk[dt][r] = dv[dt][r] = 0.f;
-
-  if (n_it > 0) {
-    stage_load(0);
-    stage_store(0);
+  for (int hi = 0; hi < 2; ++hi) {
+    const int row = 4 * h + 8 * hi + gq, f = swz(row);
+    tbase[hi] = row * 256 + 16 * ((colhalf * 2 + gch) ^ (f & 3)) + gb;
+    ttog[hi] = f >> 2;
+    kqoff[hi] = lds_off(8 * h + 4 * hi + gq, wq * 4 + colhalf * 2 + gch) + gb;
+    dsqoff[hi] = ds_off(8 * h + 4 * hi + gq, ds_unit);
   }
-  __syncthreads();
+  // dS^T stores: ds_off(l32, 2g+h) = dwbase + 16 * (g ^ dwtog)
+  const int dsx = (l32 >> 1) & 7;
+  int dwbase = l32 * 64 + 8 * (h ^ (dsx & 1)), dwtog = dsx >> 1;
+
+  f32x16_t dk[NC][4], dv[NC][4];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dk[c][dt][r] = dv[c][dt][r] = 0.f;
+
+  // K image / V rows landed before the DMA starts: consuming the V fragments here makes hipcc's own waitcnt pass
+  // retire them now instead of waiting vmcnt(0) (= draining the DMA) at their first use inside the tile loop
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) asm volatile("" : : "v"(vf[c][kk]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (n_it > 0) stage(0, 0);
+  if (n_it > 1) stage(1, 1);
+  barrier_keep_newest(n_it > 1);
 
   for (int it = 0; it < n_it; ++it) {
-    const int cur = it & 1;
-    // Lane-derived LDS offsets are recomputed every tile from a laundered lane id: hoisted out of the loop they cost
-    // ~40 registers, which at 2 waves per SIMD is the difference between spilling and not.
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int h = ln >> 5, l32 = ln & 31;
-    // transposed-read lane geometry (see flash_fwd.hip): lane reads row rb + gq, 16-B chunk c0 + 2*colhalf + gch,
-    // byte gb; it receives rows rb..rb+3 of column (lane & 31) of the addressed 32-column slab
-    const int gq = (ln >> 2) & 3, gch = (ln >> 1) & 1, gb = 8 * (ln & 1), colhalf = (ln >> 4) & 1;
-    const int ds_unit = 4 * colhalf + 2 * gch + (ln & 1);
+    const int cur = it & 1, tb = it % NBUF;
+    asm volatile("" : "+v"(rbase), "+v"(rtog), "+v"(tbase[0]), "+v"(tbase[1]), "+v"(ttog[0]), "+v"(ttog[1]),
+                 "+v"(dwbase), "+v"(dwtog), "+v"(kqoff[0]), "+v"(kqoff[1]), "+v"(dsqoff[0]), "+v"(dsqoff[1]));
     int hq, qt;
     tile_at(it, hq, qt);
     const int q0 = qt * QT;
-    if (it + 1 < n_it) stage_load(it + 1);
+    if (it + 2 < n_it) stage(it + 2, (it + 2) % NBUF);
 
-    const char* Qt = QD + cur * 2 * TILE;
+    const char* Qt = QD + tb * 2 * TILE;
     const char* Ot = Qt + TILE;
-    const float* lse2 = LD + cur * 64;
+    const float* lse2 = LD + tb * 64;
     const float* dlt = lse2 + 32;
     char* DSc = DSimg + cur * DS_BYTES;
 
-    // ---------------- does this wave's 32-key slab meet the tile? keep = bit r set if accumulator row r is unmasked
-    bool active = kw0 < S;
-    if (CAUSAL) active = active && kw0 <= q0 + QT - 1;
-    unsigned keep = mykey < S ? 0xffffu : 0u;
-    if constexpr (SPARSE) {
-      const int lh = a.lay_heads == 1 ? 0 : hq;
-      const int kbl = min(mykey, S - 1) / a.blk;
-      const uint8_t* lay = a.layout + (int64_t)lh * a.nb * a.nb;
-      const int r0 = q0 / a.blk;
-      const unsigned a0 = lay[(int64_t)r0 * a.nb + kbl] ? 0xffffu : 0u;
-      if (a.blk < QT) {  // 16-row blocks: registers 0..7 are rows 0..15 of the tile, 8..15 rows 16..31
-        const unsigned a1 = lay[(int64_t)min(r0 + 1, a.nb - 1) * a.nb + kbl] ? 0xffffu : 0u;
-        keep &= (a0 & 0x00ffu) | (a1 & 0xff00u);
-      } else {
-        keep &= a0;
+    // ---------------- which of this wave's 32-key slabs meet the tile? keep[c] bit r: accumulator row r unmasked
+    bool act[NC];
+    unsigned keep[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ks = kw0 + 32 * c, mykey = ks + l32;
+      act[c] = ks < S && (!CAUSAL || ks <= q0 + QT - 1);
+      keep[c] = mykey < S ? 0xffffu : 0u;
+      if constexpr (SPARSE) {
+        const int lh = a.lay_heads == 1 ? 0 : hq;
+        const int kbl = min(mykey, S - 1) / a.blk;
+        const uint8_t* lay = a.layout + (int64_t)lh * a.nb * a.nb;
+        const int r0 = q0 / a.blk;
+        const unsigned a0 = lay[(int64_t)r0 * a.nb + kbl] ? 0xffffu : 0u;
+        if (a.blk < QT) {  // 16-row blocks: registers 0..7 are rows 0..15 of the tile, 8..15 rows 16..31
+          const unsigned a1 = lay[(int64_t)min(r0 + 1, a.nb - 1) * a.nb + kbl] ? 0xffffu : 0u;
+          keep[c] &= (a0 & 0x00ffu) | (a1 & 0xff00u);
+        } else {
+          keep[c] &= a0;
+        }
+        act[c] = act[c] && __any(keep[c] != 0);
       }
-      active = active && __any(keep != 0);
+      if (q0 + QT > S) {  // padded query rows of the last tile
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (q0 + crow(r, h) >= S) keep[c] &= ~(1u << r);
+      }
+      if (CAUSAL && act[c] && ks + 31 > q0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (mykey > q0 + crow(r, h)) keep[c] &= ~(1u << r);
+      }
     }
-    if (active) {
+    // one 32-key slab at a time (bounds the live S / dP accumulators to 32 registers)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (!act[c] || (a.dbg & 8)) continue;
       // ---------------- S' = Q.K^T - LSE/scale and dP' = dO.V^T - delta (query rows in registers, key on the
       // lane); the row constants are the accumulators' initial values
       f32x16_t s, dp;
@@ -236,104 +344,129 @@ __global__ void __launch_bounds__(NTHR, 1) flash_bwd_kernel(BwdArgs a) {
         const f32x4 x = *reinterpret_cast<const f32x4*>(lse2 + 8 * g + 4 * h);
         const f32x4 y = *reinterpret_cast<const f32x4*>(dlt + 8 * g + 4 * h);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { s[4 * g + i] = -x[i]; dp[4 * g + i] = -y[i]; }
+        for (int i = 0; i < 4; ++i) { s[4 * g + i] = -x[i] * inv_scale; dp[4 * g + i] = -y[i]; }
       }
-      const char* Kw = Kimg + 32 * w * 256;
+      const char* Kc = Kimg + (KPW * w + 32 * c) * 256;
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(Qt + lds_off(l32, 2 * kk + h));
-        const bf16x8_t kb_ = *reinterpret_cast<const bf16x8_t*>(Kw + lds_off(l32, 2 * kk + h));
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kb_, s, 0, 0, 0);
+        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(Qt + rbase + 32 * (kk ^ rtog));
+        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(Kc + rbase + 32 * (kk ^ rtog));
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf, s, 0, 0, 0);
       }
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(Ot + lds_off(l32, 2 * kk + h));
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[kk], dp, 0, 0, 0);
+        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(Ot + rbase + 32 * (kk ^ rtog));
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[c][kk], dp, 0, 0, 0);
       }
-      // ---------------- P and dS
-      const bool need_mask = keep != 0xffffu || (CAUSAL && kw0 + 31 > q0);
-      if (CAUSAL && need_mask) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (mykey > q0 + crow(r, h)) keep &= ~(1u << r);
-      }
+      // ---------------- P and dS, dS^T -> LDS (row = key, 8-B unit g*2+h holds queries 8g+4h .. +3)
       bf16x8_t pb[2], dsb[2];
+      const bool need_mask = keep[c] != 0xffffu;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float p = __builtin_amdgcn_exp2f(s[r] * a.c);
-        if (need_mask && !((keep >> r) & 1u)) p = 0.f;
+        if (need_mask && !((keep[c] >> r) & 1u)) p = 0.f;
         pb[r >> 3][r & 7] = (bf16)p;
         dsb[r >> 3][r & 7] = (bf16)(p * dp[r]);
       }
-      // ---------------- dS^T -> LDS (row = key, 8-B unit g*2+h holds queries 8g+4h .. +3)
-      {
-        const int kr = 32 * w + l32;
+      char* dsw = DSc + (KPW * w + 32 * c) * 64;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          // whole-vector bit cast: per-element __builtin_bit_cast(short, bf16 element) is miscompiled by hipcc
-          // (ROCm 7.2) into a splat of one element (tools/probe_flash_bwd2.py)
-          const s16x8 d8 = __builtin_bit_cast(s16x8, dsb[g >> 1]);
-          s16x4 v4;
+      for (int g = 0; g < 4; ++g) {
+        // whole-vector bit cast: per-element __builtin_bit_cast(short, bf16 element) is miscompiled by hipcc
+        // (ROCm 7.2) into a splat of one element (tools/probe_flash_bwd2.py)
+        const s16x8 d8 = __builtin_bit_cast(s16x8, dsb[g >> 1]);
+        s16x4 v4;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v4[i] = d8[4 * (g & 1) + i];
-          *reinterpret_cast<s16x4*>(DSc + ds_off(kr, 2 * g + h)) = v4;
-        }
+        for (int i = 0; i < 4; ++i) v4[i] = d8[4 * (g & 1) + i];
+        *reinterpret_cast<s16x4*>(dsw + dwbase + 16 * (g ^ dwtog)) = v4;
       }
       // ---------------- dV^T += dO^T.P, dK^T += Q^T.dS   (A operands by transposed reads of the tile images)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const int ch0 = dt * 4 + colhalf * 2 + gch;
+        if (a.dbg & 4) break;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const int rb = 16 * s2 + 4 * h;
-          const bf16x8_t oT = join(tr_read(Ot + lds_off(rb + gq, ch0) + gb), tr_read(Ot + lds_off(rb + 8 + gq, ch0) + gb));
-          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oT, pb[s2], dv[dt], 0, 0, 0);
-          const bf16x8_t qT = join(tr_read(Qt + lds_off(rb + gq, ch0) + gb), tr_read(Qt + lds_off(rb + 8 + gq, ch0) + gb));
-          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, dsb[s2], dk[dt], 0, 0, 0);
+          const int t0a = tbase[0] + 64 * (dt ^ ttog[0]), t1a = tbase[1] + 64 * (dt ^ ttog[1]);
+          const bf16x8_t oT = join(tr_read(Ot + 4096 * s2 + t0a), tr_read(Ot + 4096 * s2 + t1a));
+          dv[c][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oT, pb[s2], dv[c][dt], 0, 0, 0);
+          const bf16x8_t qT = join(tr_read(Qt + 4096 * s2 + t0a), tr_read(Qt + 4096 * s2 + t1a));
+          dk[c][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, dsb[s2], dk[c][dt], 0, 0, 0);
         }
-        // bound the operand prefetch window (register budget: 2 waves per SIMD)
-        __builtin_amdgcn_sched_barrier(0);
       }
     }
     // the dQ product walks only the slabs that met this tile
-    if (lane == 0) FL[cur * NW + w] = active ? 1 : 0;
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) FL[cur * 8 + NC * w + c] = act[c] ? 1 : 0;
+    }
 
-    if (it + 1 < n_it) stage_store(cur ^ 1);
-    __syncthreads();
+    barrier_keep_newest(it + 2 < n_it);
 
-    // ---------------- dQ[q0:q0+32, 32w:32w+32] += dS . K   (waves 0..3; keys up to the diagonal)
-    if (w < 4) {
-      const uint64_t fl = *reinterpret_cast<const uint64_t*>(FL + cur * NW);
-      const uint32_t flo = __builtin_amdgcn_readfirstlane((uint32_t)fl), fhi = __builtin_amdgcn_readfirstlane((uint32_t)(fl >> 32));
+    // ---------------- dQ[q0:q0+32, 32wq:32wq+32] += dS . K over the slabs that met the tile (waves 0..3; waves
+    // 4..7 run ahead into the next tile, so the SIMDs stay busy). Measured against an even 8-wave split on
+    // 16x16x32 MFMAs: this form is 5% faster end to end (fewer transposed reads per MFMA).
+    if (w < 4 && !(a.dbg & 2)) {
+      const uint64_t fl = *reinterpret_cast<const uint64_t*>(FL + cur * 8);
+      const uint32_t flo = __builtin_amdgcn_readfirstlane((uint32_t)fl),
+                     fhi = __builtin_amdgcn_readfirstlane((uint32_t)(fl >> 32));
       f32x16_t dq;
 #pragma unroll
       for (int r = 0; r < 16; ++r) dq[r] = 0.f;
       int nks = 0;
-      const int ch0 = w * 4 + colhalf * 2 + gch;
-      for (int slab = 0; slab < NW; ++slab) {
-        if (!(((slab < 4 ? flo : fhi) >> (8 * (slab & 3))) & 0xff)) continue;
-#pragma unroll
-        for (int s2 = 2 * slab; s2 < 2 * slab + 2; ++s2) {
-          const int rb = 16 * s2 + 8 * h;
-          const bf16x8_t dsa = join(tr_read(DSc + ds_off(rb + gq, ds_unit)), tr_read(DSc + ds_off(rb + 4 + gq, ds_unit)));
-          const bf16x8_t kb_ = join(tr_read(Kimg + lds_off(rb + gq, ch0) + gb), tr_read(Kimg + lds_off(rb + 4 + gq, ch0) + gb));
-          dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dsa, kb_, dq, 0, 0, 0);
+      auto ld_a = [&](int s2) {
+        return join(tr_read(DSc + 1024 * s2 + dsqoff[0]), tr_read(DSc + 1024 * s2 + dsqoff[1]));
+      };
+      auto ld_b = [&](int s2) {
+        return join(tr_read(Kimg + 4096 * s2 + kqoff[0]), tr_read(Kimg + 4096 * s2 + kqoff[1]));
+      };
+      if constexpr (SPARSE) {
+#pragma unroll 1
+        for (int slab = 0; slab < 8; ++slab) {
+          if (!(((slab < 4 ? flo : fhi) >> (8 * (slab & 3))) & 0xff)) continue;
+          const bf16x8_t a0 = ld_a(2 * slab), b0 = ld_b(2 * slab), a1 = ld_a(2 * slab + 1), b1 = ld_b(2 * slab + 1);
+          dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, dq, 0, 0, 0);
+          dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, dq, 0, 0, 0);
+          ++nks;
         }
-        ++nks;
+      } else {
+        // keys up to the diagonal (causal) / the sequence end, as 16-key MFMA steps
+        int kmax = min(KB, S - k0);
+        if (CAUSAL) kmax = min(kmax, q0 + QT - k0);
+        nks = (kmax + 15) >> 4;
+        (void)flo;
+        (void)fhi;
+        if (nks == KB / 16) {  // every key block but the diagonal one: straight-line, scheduled by hipcc
+#pragma unroll
+          for (int s2 = 0; s2 < KB / 16; ++s2)
+            dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_a(s2), ld_b(s2), dq, 0, 0, 0);
+        } else {
+#pragma unroll 1
+          for (int s2 = 0; s2 < nks; ++s2)
+            dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_a(s2), ld_b(s2), dq, 0, 0, 0);
+        }
       }
-      if (nks > 0) {
-        float* dqp = a.dqacc + (((int64_t)b * a.Hq + hq) * S + q0) * D + 32 * w + l32;
+      if (nks > 0 && !(a.dbg & 1)) {
+        // lane part of the 16 destination rows, laundered so that hipcc forms each address next to its atomic
+        // instead of keeping 16 64-bit addresses live across the loop (they spilled). One register of a 32x32
+        // accumulator = two 128-B row segments, the full-rate atomic shape.
+        int ln = threadIdx.x;
+        asm volatile("" : "+v"(ln));
+        const int lofs = 4 * ((ln >> 5) & 1) * D + 32 * ((ln >> 6) & 3) + (ln & 31);
+        float* dqp = a.dqacc + (((int64_t)b * a.Hq + hq) * S + q0) * D + lofs;
+        const int lim = S - q0 - 4 * ((ln >> 5) & 1);  // rows (r&3) + 8(r>>2) below lim are inside the sequence
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int qr = crow(r, h);
-          if (q0 + qr < S) unsafeAtomicAdd(dqp + (int64_t)qr * D, dq[r]);
+          const int qr = (r & 3) + 8 * (r >> 2);
+          if (qr < lim) unsafeAtomicAdd(dqp + qr * D, dq[r]);
         }
       }
     }
   }
 
   // ------------------------------------------------------------------ epilogue: dK = scale * dK^T^T, dV
-  if (mykey < S) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int mykey = kw0 + 32 * c + l32;
+    if (mykey >= S) continue;
     bf16* dkp = a.dk + b * a.dksb + hk * a.dksh + (int64_t)mykey * a.dkss;
     bf16* dvp = a.dv + b * a.dvsb + hk * a.dvsh + (int64_t)mykey * a.dvss;
 #pragma unroll
@@ -343,8 +476,8 @@ __global__ void __launch_bounds__(NTHR, 1) flash_bwd_kernel(BwdArgs a) {
         bf16x4 k4, v4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          k4[i] = (bf16)(dk[dt][4 * g + i] * a.scale);
-          v4[i] = (bf16)dv[dt][4 * g + i];
+          k4[i] = (bf16)(dk[c][dt][4 * g + i] * a.scale);
+          v4[i] = (bf16)dv[c][dt][4 * g + i];
         }
         const int d0 = 32 * dt + 8 * g + 4 * h;
         *reinterpret_cast<bf16x4*>(dkp + d0) = k4;
@@ -400,19 +533,25 @@ __global__ void __launch_bounds__(256) flash_bwd_post_kernel(const float* __rest
   *reinterpret_cast<bf16x8*>(dq + bb * sb + hh * sh + (int64_t)q * ss + sub * 8) = r;
 }
 
-template <bool C, bool SP>
+template <int NW, bool C, bool SP>
 int launch_main(const BwdArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<C, SP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<NW, C, SP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<NW>());
     attr = true;
   }
   const int nkb = (a.S + KB - 1) / KB;
   const int grid = a.B * a.Hk * nkb;
-  hipLaunchKernelGGL((flash_bwd_kernel<C, SP>), dim3(grid), dim3(NTHR), LDS_BYTES, st, a);
+  hipLaunchKernelGGL((flash_bwd_kernel<NW, C, SP>), dim3(grid), dim3(NW * 64), lds_bytes<NW>(), st, a);
   DS_CHECK_LAUNCH();
   return 0;
+}
+
+template <int NW>
+int launch_mode(const BwdArgs& a, int mode, hipStream_t st) {
+  return mode == 1 ? launch_main<NW, true, false>(a, st)
+                   : (mode == 2 ? launch_main<NW, false, true>(a, st) : launch_main<NW, false, false>(a, st));
 }
 
 }  // namespace
@@ -447,9 +586,9 @@ extern "C" int ds_flash_bwd(const void* q, const void* k, const void* v, const v
   a.dvsb = dvs[0]; a.dvsh = dvs[1]; a.dvss = dvs[2];
   a.c = scale * 1.4426950408889634f;
   a.scale = scale;
+  { const char* e = getenv("DS_FLASH_BWD_DBG"); a.dbg = e ? atoi(e) : 0; }
   a.qtiles = qtiles; a.nqt = nqt; a.layout = layout; a.maxt = maxt; a.lay_heads = lay_heads; a.nb = nb; a.blk = blk;
-  int rc = mode == 1 ? launch_main<true, false>(a, st)
-                     : (mode == 2 ? launch_main<false, true>(a, st) : launch_main<false, false>(a, st));
+  int rc = launch_mode<8>(a, mode, st);
   if (rc) return rc;
   hipLaunchKernelGGL(flash_bwd_post_kernel, dim3(pgrid), dim3(256), 0, st, dqacc, (bf16*)dq, Hq, S, rows, dqs[0],
                      dqs[1], dqs[2], scale);

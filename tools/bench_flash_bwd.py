@@ -57,3 +57,12 @@ for (B, Hq, Hk, S, causal) in CONFIGS:
     print(json.dumps(res), flush=True)
     del q, k, v, do, o, lse
     torch.cuda.empty_cache()
+
+if len(sys.argv) > 1 and sys.argv[1] == "quick":
+    # pre / post passes alone (delta + zeroing, dq conversion): same traffic as inside flash_bwd
+    B, Hq, S = 8, 32, 4096
+    o = torch.randn(B, S, Hq, 128, device="cuda", dtype=torch.bfloat16).transpose(1, 2)
+    acc = torch.empty(B * Hq * S * 128, device="cuda", dtype=torch.float32)
+    t = timeit(lambda: (o.float() * o.float()).sum(-1))
+    t0 = timeit(lambda: acc.zero_())
+    print(json.dumps({"zero_dqacc_ms": round(t0, 3), "torch_delta_ms": round(t, 3)}), flush=True)
