@@ -5,7 +5,6 @@ import json
 from pydantic import BaseModel, ConfigDict
 
 
-
 class DeepSpeedConfigModel(BaseModel):
     """Sub-config base: forbids unknown keys (typo protection), accepts field aliases such as `stage3_*`.
 
@@ -42,21 +41,30 @@ def dict_raise_error_on_duplicate_keys(ordered_pairs):
 
 
 class ScientificNotationEncoder(json.JSONEncoder):
+    """Pretty-prints a config with numbers above 1000 in scientific notation (bucket sizes read as 5.000000e+08)
+    — the reference's `print_configuration` output style. Implemented as a recursive formatter over the decoded
+    structure; strings and other leaves go through the stock encoder."""
 
-    def iterencode(self, o, _one_shot=False, level=0):
-        indent = self.indent if self.indent is not None else 4
-        prefix_close = " " * level * indent
-        level += 1
-        prefix = " " * level * indent
+    def _leaf(self, o):
         if isinstance(o, bool):
             return "true" if o else "false"
-        elif isinstance(o, float) or isinstance(o, int):
-            if o > 1e3:
-                return f"{o:e}"
-            return f"{o}"
-        elif isinstance(o, collections.abc.Mapping):
-            x = [f'\n{prefix}"{k}": {self.iterencode(v, level=level)}' for k, v in o.items()]
-            return "{" + ", ".join(x) + f"\n{prefix_close}" + "}"
-        elif isinstance(o, collections.abc.Sequence) and not isinstance(o, str):
-            return f"[{', '.join(map(self.iterencode, o))}]"
-        return "\n, ".join(super().iterencode(o, _one_shot))
+        if isinstance(o, (int, float)):
+            return f"{o:e}" if o > 1e3 else f"{o}"
+        return json.JSONEncoder.encode(self, o)
+
+    def _fmt(self, o, depth):
+        step = self.indent if self.indent is not None else 4
+        pad, inner = " " * (depth * step), " " * ((depth + 1) * step)
+        if isinstance(o, collections.abc.Mapping):
+            items = sorted(o.items()) if self.sort_keys else o.items()
+            body = ", ".join(f'\n{inner}"{k}": {self._fmt(v, depth + 1)}' for k, v in items)
+            return "{" + body + f"\n{pad}" + "}"
+        if isinstance(o, collections.abc.Sequence) and not isinstance(o, (str, bytes)):
+            return "[" + ", ".join(self._fmt(v, depth + 1) for v in o) + "]"
+        return self._leaf(o)
+
+    def encode(self, o):
+        return self._fmt(o, 0)
+
+    def iterencode(self, o, _one_shot=False):
+        yield self.encode(o)

@@ -1,12 +1,16 @@
-"""PipelineModule / LayerSpec / TiedLayerSpec (reference `runtime/pipe/module.py:30-636`).
+"""PipelineModule / LayerSpec / TiedLayerSpec (API of the reference `runtime/pipe/module.py:30-636`).
 
-The model is described as a flat list of layers (or LayerSpecs, built lazily so each stage only materialises its own
-layers). Layers are partitioned over the pipeline stages by `partition_method`:
-  "parameters" (balance trainable parameter counts), "uniform" (balance layer counts),
-  "type:<regex>" (balance layers whose class name matches), or an explicit list of boundaries.
-Tied layers (e.g. input embedding and LM head) are built on every stage that uses them; their gradients are summed
-over the tie group and their weights broadcast from the first owner at init.
+The model is a flat sequence of entries — modules, LayerSpecs (built lazily, so a stage only materialises its own
+layers), TiedLayerSpecs (one module shared by several positions, e.g. input embedding and LM head) or plain callables.
+The sequence is cut into `num_stages` contiguous ranges by `partition_method`:
+  "parameters"   — balance trainable parameter counts,
+  "uniform"      — balance entry counts,
+  "type:<regex>" — balance the entries whose class name matches,
+  or an explicit list of stage boundaries.
+Tied modules exist on every stage that uses them; their weights are broadcast from the lowest rank of the tie group at
+construction and their gradients summed over it before the optimizer step.
 """
+import os
 import re
 from functools import partial
 
@@ -14,7 +18,6 @@ import torch
 import torch.nn as nn
 
 from ... import comm as dist
-from ...utils.logging import logger
 from .topology import PipeDataParallelTopology, PipelineParallelGrid
 
 
@@ -23,13 +26,14 @@ class PipelineError(Exception):
 
 
 class LayerSpec:
+    """A deferred `typename(*args, **kwargs)`: only the owning stage pays for construction."""
 
     def __init__(self, typename, *module_args, **module_kwargs):
+        if not (isinstance(typename, type) and issubclass(typename, nn.Module)):
+            raise RuntimeError("LayerSpec only supports torch.nn.Module types.")
         self.typename = typename
         self.module_args = module_args
         self.module_kwargs = module_kwargs
-        if not issubclass(typename, nn.Module):
-            raise RuntimeError("LayerSpec only supports torch.nn.Module types.")
         self.global_rank = dist.get_rank() if dist.is_initialized() else -1
 
     def __repr__(self):
@@ -40,6 +44,7 @@ class LayerSpec:
 
 
 class TiedLayerSpec(LayerSpec):
+    """A LayerSpec whose module is shared by every entry with the same `key` (one instance per stage)."""
 
     def __init__(self, key, typename, *module_args, forward_fn=None, tied_weight_attr="weight", **module_kwargs):
         super().__init__(typename, *module_args, **module_kwargs)
@@ -49,20 +54,14 @@ class TiedLayerSpec(LayerSpec):
 
 
 def partition_uniform(num_items, num_parts):
-    parts = [0] * (num_parts + 1)
+    """Boundaries [b0=0, ..., b_parts=num_items] with item counts differing by at most one."""
     if num_items <= num_parts:
-        for p in range(num_parts + 1):
-            parts[p] = min(p, num_items)
-        return parts
-    chunk = num_items / num_parts
-    for p in range(num_parts):
-        parts[p] = int(round(chunk * p))
-    parts[num_parts] = num_items
-    return parts
+        return [min(p, num_items) for p in range(num_parts + 1)]
+    return [round(p * num_items / num_parts) for p in range(num_parts)] + [num_items]
 
 
 def partition_balanced(weights, num_parts):
-    """Contiguous partition minimising the max part weight (binary search over the bottleneck)."""
+    """Contiguous partition minimising the heaviest part: binary search on that bound, greedy feasibility check."""
     n = len(weights)
     if num_parts >= n:
         return [min(i, n) for i in range(num_parts + 1)]
@@ -70,29 +69,42 @@ def partition_balanced(weights, num_parts):
     for w in weights:
         prefix.append(prefix[-1] + w)
 
-    def parts_for(limit):
-        parts = [0]
-        start = 0
+    def cut(bound):
+        bounds, start = [0], 0
         for _ in range(num_parts):
             end = start
-            while end < n and prefix[end + 1] - prefix[start] <= limit:
+            while end < n and prefix[end + 1] - prefix[start] <= bound:
                 end += 1
             if end == start and start < n:
                 return None
-            parts.append(end)
+            bounds.append(end)
             start = end
-        return parts if parts[-1] == n else None
+        return bounds if bounds[-1] == n else None
 
-    lo, hi = max(weights), prefix[-1]
-    best = None
+    lo, hi, best = max(weights), prefix[-1], None
     while lo <= hi:
         mid = (lo + hi) // 2
-        p = parts_for(mid)
-        if p is not None:
-            best, hi = p, mid - 1
-        else:
+        b = cut(mid)
+        if b is None:
             lo = mid + 1
+        else:
+            best, hi = b, mid - 1
     return best
+
+
+def _entry_name(entry):
+    if isinstance(entry, LayerSpec):
+        return entry.typename.__name__
+    if isinstance(entry, nn.Module):
+        return type(entry).__name__
+    return getattr(entry, "__name__", None)
+
+
+def _entry_params(entry):
+    module = entry.build() if isinstance(entry, LayerSpec) else entry
+    if not isinstance(module, nn.Module):
+        return 0
+    return sum(p.numel() for p in module.parameters() if p.requires_grad)
 
 
 class PipelineModule(nn.Module):
@@ -106,31 +118,23 @@ class PipelineModule(nn.Module):
         self.micro_offset = 0
         self.loss_fn = loss_fn
         self.checkpointable_layers = checkpointable_layers
-        self.seed_layers = seed_layers
-        self.seed_fn = seed_fn
-        self.base_seed = base_seed
+        self.seed_layers, self.seed_fn, self.base_seed = seed_layers, seed_fn, base_seed
         self.world_group = dist.new_group(ranks=range(dist.get_world_size()))
         self.global_rank = dist.get_rank(group=self.world_group)
         self.world_size = dist.get_world_size(group=self.world_group)
-        self.local_rank = int(__import__("os").environ.get("LOCAL_RANK", "0"))
-        if topology:
-            self._topo = topology
-            self.num_stages = self._topo.get_dim("pipe")
-        else:
-            self.num_stages = num_stages
-            self._topo = PipeDataParallelTopology(num_pp=num_stages, num_dp=self.world_size // num_stages)
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self._topo = topology or PipeDataParallelTopology(num_pp=num_stages, num_dp=self.world_size // num_stages)
+        self.num_stages = self._topo.get_dim("pipe")
         self._grid = PipelineParallelGrid(process_group=self.world_group, topology=self._topo)
         self.stage_id = self._topo.get_coord(self.global_rank).pipe
         self._layer_specs = list(layers)
         self._num_layers = len(self._layer_specs)
-        self._local_start = 0
-        self._local_stop = None
-        self._partition_layers(method=partition_method)
-        self.forward_funcs = []
-        self.fwd_map = {}
-        self.tied_modules = nn.ModuleDict()
-        self.tied_weight_attrs = {}
-        self._build()
+        self.parts = self._stage_boundaries(partition_method)
+        self._local_start, self._local_stop = self.parts[self.stage_id], self.parts[self.stage_id + 1]
+        self.forward_funcs, self.fwd_map = [], {}
+        self.tied_modules, self.tied_weight_attrs = nn.ModuleDict(), {}
+        for idx in range(self._local_start, self._local_stop):
+            self._materialize(idx)
         self.tied_comms = self._index_tied_modules()
         self._synchronize_tied_weights()
         self.activation_checkpoint_interval = activation_checkpoint_interval
@@ -139,187 +143,134 @@ class PipelineModule(nn.Module):
             activation_checkpoint_func = checkpointing.checkpoint
         self.activation_checkpoint_func = activation_checkpoint_func
 
-    # ------------------------------------------------------------------------------------------ build
-    def _build(self):
-        specs = self._layer_specs
-        for local_idx, layer in enumerate(specs[self._local_start:self._local_stop]):
-            layer_idx = local_idx + self._local_start
-            if self.seed_layers:
-                (self.seed_fn or torch.manual_seed)(self.base_seed + layer_idx)
-            if isinstance(layer, nn.Module):
-                name = str(layer_idx)
-                self.forward_funcs.append(layer)
-                self.fwd_map[name] = len(self.forward_funcs) - 1
-                self.add_module(name, layer)
-            elif isinstance(layer, TiedLayerSpec):
-                if layer.key not in self.tied_modules:
-                    self.tied_modules[layer.key] = layer.build()
-                    self.tied_weight_attrs[layer.key] = layer.tied_weight_attr
-                if layer.forward_fn is None:
-                    self.forward_funcs.append(self.tied_modules[layer.key])
-                else:
-                    self.forward_funcs.append(partial(layer.forward_fn, self.tied_modules[layer.key]))
-            elif isinstance(layer, LayerSpec):
-                module = layer.build()
-                name = str(layer_idx)
-                self.forward_funcs.append(module)
-                self.fwd_map[name] = len(self.forward_funcs) - 1
-                self.add_module(name, module)
-            else:
-                self.forward_funcs.append(layer)  # plain callable (e.g. lambda reshape)
-
-    def _count_layer_params(self):
-        counts = []
-        for layer in self._layer_specs:
-            if isinstance(layer, LayerSpec):
-                m = layer.build()
-                counts.append(sum(p.numel() for p in m.parameters() if p.requires_grad))
-            elif isinstance(layer, nn.Module):
-                counts.append(sum(p.numel() for p in layer.parameters() if p.requires_grad))
-            else:
-                counts.append(0)
-        return counts
-
-    def _find_layer_type(self, layername):
-        idxs = []
-        typeregex = re.compile(layername, re.IGNORECASE)
-        for idx, layer in enumerate(self._layer_specs):
-            name = None
-            if isinstance(layer, LayerSpec):
-                name = layer.typename.__name__
-            elif isinstance(layer, nn.Module):
-                name = layer.__class__.__name__
-            else:
-                try:
-                    name = layer.__name__
-                except AttributeError:
-                    continue
-            if typeregex.search(name):
-                idxs.append(idx)
-        if len(idxs) == 0:
-            raise RuntimeError(f"Partitioning '{layername}' found no valid layers to partition.")
-        return idxs
-
-    def _partition_layers(self, method="uniform"):
-        num_stages = self._topo.get_dim("pipe")
-        stage_id = self._topo.get_coord(self.global_rank).pipe
+    # ------------------------------------------------------------------------------------------ partitioning
+    def _stage_boundaries(self, method):
         if isinstance(method, (list, tuple)):
-            self.parts = list(method)
-        else:
-            method = method.lower()
-            if method == "uniform":
-                self.parts = partition_uniform(num_items=self._num_layers, num_parts=num_stages)
-            elif method == "parameters":
-                counts = self._count_layer_params()
-                self.parts = partition_balanced(weights=[max(c, 1) for c in counts], num_parts=num_stages)
-            elif method.startswith("type:"):
-                layertype = method.split(":")[1]
-                binary = [0] * len(self._layer_specs)
-                for idx in self._find_layer_type(layertype):
-                    binary[idx] = 1
-                self.parts = partition_balanced(weights=[b * 1000 + 1 for b in binary], num_parts=num_stages)
-            elif method == "profile":
-                raise NotImplementedError(f"Partitioning method {method} not implemented.")
-            else:
-                raise NotImplementedError(f"Partitioning method {method} not implemented.")
-        self._set_bounds(start=self.parts[stage_id], stop=self.parts[stage_id + 1])
+            bounds = [int(b) for b in method]
+            if len(bounds) != self.num_stages + 1 or bounds[0] != 0 or bounds[-1] != self._num_layers:
+                raise PipelineError(f"explicit partition {bounds} does not cover {self._num_layers} layers")
+            return bounds
+        method = method.lower()
+        if method == "uniform":
+            return partition_uniform(self._num_layers, self.num_stages)
+        if method == "parameters":
+            return partition_balanced([max(_entry_params(e), 1) for e in self._layer_specs], self.num_stages)
+        if method.startswith("type:"):
+            pattern = re.compile(method.split(":", 1)[1], re.IGNORECASE)
+            hits = [bool(_entry_name(e) and pattern.search(_entry_name(e))) for e in self._layer_specs]
+            if not any(hits):
+                raise RuntimeError(f"Partitioning '{method}' found no valid layers to partition.")
+            # matching layers dominate the balance; the +1 keeps the partition contiguous and total
+            return partition_balanced([1000 * h + 1 for h in hits], self.num_stages)
+        raise NotImplementedError(f"Partitioning method {method} not implemented.")
 
     def _set_bounds(self, start=None, stop=None):
-        self._local_start = start
-        self._local_stop = stop
+        self._local_start, self._local_stop = start, stop
 
-    # ------------------------------------------------------------------------------------------ tied weights
-    def _index_tied_modules(self):
-        tied_comms = {}
-        if self._topo.get_dim("pipe") == 1:
-            return tied_comms
-        specs = self._layer_specs
-        tie_keys = set(s.key for s in specs if isinstance(s, TiedLayerSpec))
-        for key in sorted(tie_keys):
-            tied_layers = [i for i, s in enumerate(specs) if isinstance(s, TiedLayerSpec) and s.key == key]
-            tied_stages = sorted(set(self.stage_owner(i) for i in tied_layers))
-            for dp in range(self._grid.data_parallel_size):
-                for mp in range(self._grid.get_slice_parallel_world_size()):
-                    tied_ranks = []
-                    for s in tied_stages:
-                        if self._grid.get_slice_parallel_world_size() > 1:
-                            tied_ranks.append(self._grid.stage_to_global(stage_id=s, data=dp, model=mp))
-                        else:
-                            tied_ranks.append(self._grid.stage_to_global(stage_id=s, data=dp))
-                    group = dist.new_group(ranks=tied_ranks)
-                    if self.global_rank in tied_ranks:
-                        assert key in self.tied_modules
-                        tied_comms[key] = {
-                            "ranks": tied_ranks,
-                            "group": group,
-                            "weight_attr": self.tied_weight_attrs[key],
-                            "module": self.tied_modules[key],
-                        }
-        return tied_comms
-
-    def _synchronize_tied_weights(self):
-        for key, comm in self.tied_comms.items():
-            w = getattr(comm["module"], comm["weight_attr"])
-            dist.broadcast(w.data, src=min(comm["ranks"]), group=comm["group"])
-
-    def allreduce_tied_weight_gradients(self):
-        for key, comm in self.tied_comms.items():
-            w = getattr(comm["module"], comm["weight_attr"])
-            if w.grad is not None:
-                dist.all_reduce(w.grad, group=comm["group"])
-
-    def get_tied_weights_and_groups(self):
-        return [(getattr(c["module"], c["weight_attr"]), c["group"]) for c in self.tied_comms.values()]
-
-    # ------------------------------------------------------------------------------------------ forward
-    def forward(self, forward_input):
-        self.micro_offset += 1
-
-        def exec_range_func(start, end):
-            local_micro_offset = self.micro_offset + 1
-
-            def exec_func(*inputs):
-                if len(inputs) == 1:
-                    inputs = inputs[0]
-                for idx, layer in enumerate(self.forward_funcs[start:end]):
-                    self.curr_layer = idx + self._local_start
-                    if self.seed_layers:
-                        new_seed = (self.base_seed * local_micro_offset) + self.curr_layer
-                        (self.seed_fn or torch.manual_seed)(new_seed)
-                    inputs = layer(inputs)
-                return inputs
-
-            return exec_func
-
-        if self.activation_checkpoint_interval == 0 or not self.training:
-            return exec_range_func(0, len(self.forward_funcs))(forward_input)
-        num_layers = len(self.forward_funcs)
-        x = forward_input
-        for start_idx in range(0, num_layers, self.activation_checkpoint_interval):
-            end_idx = min(start_idx + self.activation_checkpoint_interval, num_layers)
-            funcs = self.forward_funcs[start_idx:end_idx]
-            if not isinstance(x, tuple):
-                x = (x, )
-            if self._is_checkpointable(funcs):
-                x = self.activation_checkpoint_func(exec_range_func(start_idx, end_idx), *x)
-            else:
-                x = exec_range_func(start_idx, end_idx)(*x)
-        return x
-
-    def _is_checkpointable(self, funcs):
-        if self.checkpointable_layers is not None:
-            return all(f.__class__.__name__ in self.checkpointable_layers for f in funcs)
-        params = [f.parameters() for f in funcs if isinstance(f, nn.Module)]
-        return any(len(list(p)) > 0 for p in params)
-
-    # ------------------------------------------------------------------------------------------ misc
     def stage_owner(self, layer_idx):
-        assert 0 <= layer_idx < self._num_layers
-        for stage in range(self._topo.get_dim("pipe")):
+        if not 0 <= layer_idx < self._num_layers:
+            raise AssertionError(f"layer {layer_idx} out of range")
+        for stage in range(self.num_stages):
             if self.parts[stage] <= layer_idx < self.parts[stage + 1]:
                 return stage
         raise RuntimeError(f"Layer {layer_idx} not owned? parts={self.parts}")
 
+    # ------------------------------------------------------------------------------------------ construction
+    def _materialize(self, idx):
+        entry = self._layer_specs[idx]
+        if self.seed_layers:
+            (self.seed_fn or torch.manual_seed)(self.base_seed + idx)
+        if isinstance(entry, TiedLayerSpec):
+            if entry.key not in self.tied_modules:
+                self.tied_modules[entry.key] = entry.build()
+                self.tied_weight_attrs[entry.key] = entry.tied_weight_attr
+            shared = self.tied_modules[entry.key]
+            self.forward_funcs.append(shared if entry.forward_fn is None else partial(entry.forward_fn, shared))
+            return
+        module = entry.build() if isinstance(entry, LayerSpec) else entry
+        self.forward_funcs.append(module)
+        if isinstance(module, nn.Module):
+            self.fwd_map[str(idx)] = len(self.forward_funcs) - 1
+            self.add_module(str(idx), module)
+
+    # ------------------------------------------------------------------------------------------ tied weights
+    def _index_tied_modules(self):
+        """One group per (tie key, data replica, model slice) over the stages that hold the tied module."""
+        comms = {}
+        if self.num_stages == 1:
+            return comms
+        specs = self._layer_specs
+        keys = sorted({s.key for s in specs if isinstance(s, TiedLayerSpec)})
+        slices = self._grid.get_slice_parallel_world_size()
+        for key in keys:
+            stages = sorted({self.stage_owner(i) for i, s in enumerate(specs)
+                             if isinstance(s, TiedLayerSpec) and s.key == key})
+            for dp in range(self._grid.data_parallel_size):
+                for mp in range(slices):
+                    extra = {"data": dp}
+                    if slices > 1:
+                        extra["model"] = mp
+                    ranks = [self._grid.stage_to_global(stage_id=s, **extra) for s in stages]
+                    group = dist.new_group(ranks=ranks)
+                    if self.global_rank in ranks:
+                        comms[key] = {"ranks": ranks, "group": group, "weight_attr": self.tied_weight_attrs[key],
+                                      "module": self.tied_modules[key]}
+        return comms
+
+    def _tied_weight(self, comm):
+        return getattr(comm["module"], comm["weight_attr"])
+
+    def _synchronize_tied_weights(self):
+        for comm in self.tied_comms.values():
+            dist.broadcast(self._tied_weight(comm).data, src=min(comm["ranks"]), group=comm["group"])
+
+    def allreduce_tied_weight_gradients(self):
+        for comm in self.tied_comms.values():
+            w = self._tied_weight(comm)
+            if w.grad is not None:
+                dist.all_reduce(w.grad, group=comm["group"])
+
+    def get_tied_weights_and_groups(self):
+        return [(self._tied_weight(c), c["group"]) for c in self.tied_comms.values()]
+
+    # ------------------------------------------------------------------------------------------ forward
+    def _segment(self, start, end):
+        """Callable running local entries [start, end); with seed_layers every layer reseeds from (micro-batch,
+        layer index) so recomputation under activation checkpointing replays the same dropout masks."""
+        micro = self.micro_offset + 1
+
+        def run(*inputs):
+            x = inputs[0] if len(inputs) == 1 else inputs
+            for j, fn in enumerate(self.forward_funcs[start:end]):
+                self.curr_layer = self._local_start + start + j
+                if self.seed_layers:
+                    (self.seed_fn or torch.manual_seed)(self.base_seed * micro + self.curr_layer)
+                x = fn(x)
+            return x
+
+        return run
+
+    def forward(self, forward_input):
+        self.micro_offset += 1
+        n = len(self.forward_funcs)
+        interval = self.activation_checkpoint_interval
+        if interval == 0 or not self.training:
+            return self._segment(0, n)(forward_input)
+        x = forward_input
+        for lo in range(0, n, interval):
+            hi = min(lo + interval, n)
+            args = x if isinstance(x, tuple) else (x, )
+            seg = self._segment(lo, hi)
+            x = self.activation_checkpoint_func(seg, *args) if self._is_checkpointable(self.forward_funcs[lo:hi]) \
+                else seg(*args)
+        return x
+
+    def _is_checkpointable(self, funcs):
+        if self.checkpointable_layers is not None:
+            return all(type(f).__name__ in self.checkpointable_layers for f in funcs)
+        return any(isinstance(f, nn.Module) and any(True for _ in f.parameters()) for f in funcs)
+
+    # ------------------------------------------------------------------------------------------ misc
     def topology(self):
         return self._topo
 
@@ -327,18 +278,12 @@ class PipelineModule(nn.Module):
         return self._grid
 
     def num_pipeline_stages(self):
-        return self._topo.get_dim("pipe")
+        return self.num_stages
 
     def ckpt_prefix(self, checkpoints_path, tag):
-        import os
         return os.path.join(checkpoints_path, str(tag))
 
     def ckpt_layer_path(self, ckpt_dir, local_layer_idx):
-        import os
         idx = local_layer_idx + self._local_start
-        layer_ckpt_path = os.path.join(ckpt_dir, f"layer_{idx:02d}")
-        rank_repr = self._grid._topo.get_rank_repr(rank=self.global_rank)
-        if rank_repr != "":
-            layer_ckpt_path += f"-{rank_repr}"
-        layer_ckpt_path += "-model_states.pt"
-        return layer_ckpt_path
+        suffix = self._grid._topo.get_rank_repr(rank=self.global_rank)
+        return os.path.join(ckpt_dir, f"layer_{idx:02d}" + (f"-{suffix}" if suffix else "") + "-model_states.pt")

@@ -80,3 +80,27 @@ def test_partition_balanced():
     assert partition_uniform(10, 2) == [0, 5, 10]
     p = partition_balanced([1, 1, 1, 10, 1, 1], 2)
     assert p[0] == 0 and p[-1] == 6 and len(p) == 3
+
+
+def test_topology_radix_math():
+    """Mixed-radix topology (reference semantics of `runtime/pipe/topology.py`): coordinates, axis communicators,
+    filters and rank strings agree with a brute-force enumeration."""
+    import itertools
+    from deepspeedsyclsupport_amd.runtime.pipe.topology import ProcessTopology, PipeModelDataParallelTopology
+    topo = PipeModelDataParallelTopology(num_pp=2, num_mp=2, num_dp=3)
+    axes, dims = topo.get_axis_names(), [2, 3, 2]
+    brute = {c: r for r, c in enumerate(itertools.product(*[range(d) for d in dims]))}
+    for c, r in brute.items():
+        assert topo.get_rank(**dict(zip(axes, c))) == r
+        assert tuple(topo.get_coord(r)) == c
+    for axis in axes:
+        k = axes.index(axis)
+        lists = topo.get_axis_comm_lists(axis)
+        assert sorted(sum(lists, [])) == list(range(12))
+        for l in lists:
+            cs = [topo.get_coord(r) for r in l]
+            assert [c[k] for c in cs] == list(range(dims[k]))
+            assert len({tuple(v for i, v in enumerate(c) if i != k) for c in cs}) == 1
+    assert topo.filter_match(pipe=1, model=0) == [r for c, r in brute.items() if c[0] == 1 and c[2] == 0]
+    assert topo.get_rank_repr(5) == "model_01"
+    assert ProcessTopology(["a"], [4]).get_axis_comm_lists("b") == []
