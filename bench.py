@@ -226,6 +226,10 @@ def main():
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{dp}" + (f"-sp{args.sp}" if args.sp > 1 else ""),
                 "zero_stage": args.stage,
+                # True when parameters / gradients really are partitioned and gathered / reduce-scattered in the
+                # timed steps (always with > 1 data-parallel rank; at one rank only with DS_ZERO_FORCE_PARTITION=1)
+                "zero_partitioned": bool(getattr(engine.optimizer, "partition", False)),
+                "attention": "in-tree CDNA4 flash fwd+bwd (csrc/attn/flash_{fwd,bwd}.hip)",
                 "micro_batch_per_gpu": args.micro_batch,
                 "gradient_accumulation_steps": args.gas,
                 "activation_checkpointing": bool(args.ckpt),
