@@ -6,8 +6,10 @@ can swap in oneCCL; on MI355X there is one backend — torch.distributed with `n
 tensors and `gloo` on the host path — so this module calls torch.distributed directly and only adds:
   * `timed_op` comms logging (algbw/busbw + per-xGMI-link figure),
   * process-group bookkeeping for `get_world_group`, `new_group`,
-  * coalesced helpers used by ZeRO (`all_gather_coalesced`, `reduce_scatter_coalesced` live in
-    `runtime/comm/coalesced_collectives.py`).
+  * `inference_all_reduce` over the native small-message paths of `comm/xgmi.py` (xGMI peer-mapped kernel for
+    device tensors, POSIX shm for host tensors).
+The ZeRO bucketed collectives (the reference's `runtime/comm/coalesced_collectives.py`) are issued directly by the
+flat-group optimizer (`runtime/zero/flat_optimizer.py`, `runtime/zero/zeropp.py`).
 """
 import functools
 import os
@@ -234,7 +236,13 @@ def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, **kw):
 
 @timed_op
 def inference_all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, **kw):
-    # small-message TP all-reduce; the native xGMI one-shot path lives in ops/comm (used when available)
+    """Tensor-parallel decode all-reduce (reference `deepspeed/comm/comm.py` inference_all_reduce). SUM over one
+    node takes the native paths of `comm/xgmi.py` — peer-mapped xGMI kernel for device tensors (capturable, no host
+    sync), POSIX-shm reduce for host tensors — and falls back to RCCL / gloo otherwise."""
+    if op == ReduceOp.SUM and not async_op and is_initialized():
+        from . import xgmi
+        if xgmi.fast_all_reduce(tensor, group):
+            return None
     return tdist.all_reduce(tensor, op=op, group=group, async_op=async_op)
 
 

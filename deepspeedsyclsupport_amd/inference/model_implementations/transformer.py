@@ -89,15 +89,21 @@ def alibi_slopes(n_heads):
 
 
 class QuantLinearWeight:
-    """Group-quantised weight (int8/int4) dequantised into a shared workspace right before its GEMM."""
+    """Group-quantised weight (int8/int4). Symmetric int8 with K a multiple of 64 is kept pre-shuffled for the decode
+    MFMA stream (`ops/int8_gemv.py`); everything else is dequantised into a temporary right before its GEMM."""
 
     def __init__(self, w, bits=8, group_size=64):
+        from ...ops.int8_gemv import Int8Weight
         from ...ops.quantizer import quantize
         self.shape = w.shape
         self.dtype = w.dtype
-        self.qt = quantize(w, group_size=min(group_size, w.numel()), bits=bits, symmetric=True)
+        self.i8 = Int8Weight(w, group_size) if Int8Weight.supported(w, bits, group_size) else None
+        self.qt = None if self.i8 is not None else \
+            quantize(w, group_size=min(group_size, w.numel()), bits=bits, symmetric=True)
 
     def materialize(self):
+        if self.i8 is not None:
+            return self.i8.materialize()
         from ...ops.quantizer import dequantize
         return dequantize(self.qt, self.dtype)
 
@@ -164,20 +170,13 @@ class DSInferenceLayer(nn.Module):
                                                    device=getattr(self, name).device)
 
     def _linear(self, x, name, bias=None):
-        """x . W^T (+ bias). Int8 weight-only layers at decode sizes (<= 16 token rows) run the fused-dequant skinny
-        kernels (`csrc/gemv/skinny_int8.hip`: stream int8 + group scales into VALU FMAs for one row, into MFMAs
-        for 2-16 rows; never materialise a bf16 weight);
-        everything else dequantises into a bf16 temporary for a library GEMM (reference `ds_vector_matmul_int8`)."""
+        """x . W^T (+ bias). Int8 weight-only layers run `Int8Weight.linear`: at decode sizes (<= 16 token rows) the
+        fused-dequant MFMA stream over the pre-shuffled weight (`csrc/gemv/skinny_int8.hip`, never materialises a
+        bf16 weight); larger batches dequantise into a bf16 temporary for a library GEMM (reference
+        `ds_vector_matmul_int8`)."""
         qw = self.quant.get(name)
-        if qw is not None and x.is_cuda and x.dtype == torch.bfloat16 and qw.qt.bits == 8 \
-                and qw.qt.zeros.numel() == 0 and len(qw.shape) == 2:
-            from ...ops.native import hip_ops
-            K = x.shape[-1]
-            M = x.numel() // K
-            if hip_ops().skinny_i8_ok(M, K, qw.qt.group_size):
-                y = hip_ops().skinny_i8(x.reshape(M, K).contiguous(), qw.qt.data, qw.qt.scales, bias, qw.shape[0],
-                                        qw.qt.group_size)
-                return y.view(*x.shape[:-1], qw.shape[0])
+        if qw is not None and qw.i8 is not None:
+            return qw.i8.linear(x, bias)
         return F.linear(x, self._w(name), bias)
 
     def _w(self, name):

@@ -4,7 +4,9 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime_api.h>
 
+#include <map>
 #include <optional>
+#include <utility>
 
 extern "C" {
 int ds_paged_decode_splits(int, int, int);
@@ -23,7 +25,10 @@ int ds_kv_append(const void*, const void*, void*, void*, const int*, const int*,
                  hipStream_t);
 int ds_skinny_i8_ok(int, int, int);
 int ds_skinny_i8_mfma_ok(int, int, int);
-int ds_skinny_i8_mfma(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
+int ds_skinny_i8_mfma(const void*, const int8_t*, const float*, const void*, void*, float*, int, int, int, int,
+                      hipStream_t);
+int64_t ds_skinny_i8_mfma_ws_floats(int);
+void ds_skinny_i8_tune(int, int, int);
 int ds_skinny_i8(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
 int ds_quantize(const void*, int8_t*, float*, float*, int64_t, int, int, int, int, unsigned, int, hipStream_t);
 int ds_dequantize(const int8_t*, const float*, const float*, void*, int64_t, int, int, int, int, hipStream_t);
@@ -220,22 +225,33 @@ std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, 
   return {q};
 }
 
-bool skinny_i8_ok(int64_t M, int64_t K, int64_t gs) {
-  return ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0 || ds_skinny_i8_mfma_ok((int)M, (int)K, (int)gs) != 0;
+// Self-cleaning split-K workspace of the MFMA path (zero between calls: the kernel re-zeroes what it used), one per
+// (device, stream) so concurrent streams never share partial sums; grown (never shrunk) on demand.
+struct I8Workspace {
+  Tensor acc;
+};
+std::map<std::pair<int, hipStream_t>, I8Workspace>& i8_workspaces() {
+  static std::map<std::pair<int, hipStream_t>, I8Workspace> m;
+  return m;
+}
+I8Workspace& i8_workspace(const Tensor& like, int64_t N) {
+  auto& ws = i8_workspaces()[{like.get_device(), stream()}];
+  const int64_t nf = ds_skinny_i8_mfma_ws_floats((int)N);
+  if (!ws.acc.defined() || ws.acc.numel() < nf) ws.acc = torch::zeros({nf}, like.options().dtype(at::kFloat));
+  return ws;
 }
 
-// x [M, K] bf16 (M <= 8), q int8 [N * K] (row-major [N, K], symmetric), scales fp32 [N * K / gs] -> y [M, N] bf16
-Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_t gs, int64_t path) {
+bool skinny_i8_ok(int64_t M, int64_t K, int64_t gs) { return ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0; }
+bool skinny_i8_sh_ok(int64_t M, int64_t K, int64_t gs) { return ds_skinny_i8_mfma_ok((int)M, (int)K, (int)gs) != 0; }
+
+// VALU stream over a row-major weight: x [M, K] bf16 (M <= 8), q int8 [N * K] (symmetric), scales fp32
+// [N * K / gs] -> y [M, N] bf16
+Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_t gs) {
   need(x, "x"); need(q, "q"); need(scales, "scales");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "skinny_i8: x must be bf16 [M, K]");
   TORCH_CHECK(q.scalar_type() == at::kChar && scales.scalar_type() == at::kFloat, "skinny_i8: int8 q, fp32 scales");
   const int64_t M = x.size(0), K = x.size(1);
-  // path: 1 = VALU stream (M <= 8), 2 = MFMA (M <= 16, K and gs multiples of 64); 0 = pick (VALU up to 3 rows)
-  const bool valu_ok = ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0;
-  const bool mfma_ok = ds_skinny_i8_mfma_ok((int)M, (int)K, (int)gs) != 0;
-  // measured (tools/bench_int8_gemv.py): VALU 6.1-6.4 TB/s at 1 row, ~3 at 4 rows; MFMA ~3 TB/s flat to 8 rows
-  const bool use_mfma = path == 2 || (path == 0 && mfma_ok && (M > 3 || !valu_ok));
-  TORCH_CHECK(use_mfma ? mfma_ok : valu_ok, "skinny_i8: unsupported shape for the requested path (M ", M, ", K ", K,
+  TORCH_CHECK(ds_skinny_i8_ok((int)M, (int)K, (int)gs) != 0, "skinny_i8: unsupported shape (M ", M, ", K ", K,
               ", gs ", gs, ")");
   TORCH_CHECK(q.numel() == N * K && scales.numel() == N * K / gs, "skinny_i8: q / scales size");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
@@ -247,21 +263,48 @@ Tensor skinny_i8(Tensor x, Tensor q, Tensor scales, OptT bias, int64_t N, int64_
     bp = bias->data_ptr();
   }
   auto y = torch::empty({M, N}, x.options());
-  if (use_mfma)
-    check(ds_skinny_i8_mfma(x.data_ptr(), q.data_ptr<int8_t>(), scales.data_ptr<float>(), bp, y.data_ptr(), (int)M,
-                            (int)N, (int)K, (int)gs, stream()),
-          "skinny_i8_mfma");
-  else
-    check(ds_skinny_i8(x.data_ptr(), q.data_ptr<int8_t>(), scales.data_ptr<float>(), bp, y.data_ptr(), (int)M,
-                       (int)N, (int)K, (int)gs, stream()),
-          "skinny_i8");
+  check(ds_skinny_i8(x.data_ptr(), q.data_ptr<int8_t>(), scales.data_ptr<float>(), bp, y.data_ptr(), (int)M, (int)N,
+                     (int)K, (int)gs, stream()),
+        "skinny_i8");
+  return y;
+}
+
+// MFMA stream over the pre-shuffled layout (ops/int8_gemv.py: preshuffle): x [M, K] bf16 (M <= 16),
+// qsh int8 [ceil(N/16), K/64, 64, 16], ssh fp32 [ceil(N/16), K/gs, 16] -> y [M, N] bf16
+Tensor skinny_i8_sh(Tensor x, Tensor qsh, Tensor ssh, OptT bias, int64_t N, int64_t gs) {
+  need(x, "x"); need(qsh, "qsh"); need(ssh, "ssh");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "skinny_i8_sh: x must be bf16 [M, K]");
+  TORCH_CHECK(qsh.scalar_type() == at::kChar && ssh.scalar_type() == at::kFloat, "skinny_i8_sh: int8 q, fp32 scales");
+  const int64_t M = x.size(0), K = x.size(1), NB = (N + 15) / 16;
+  TORCH_CHECK(ds_skinny_i8_mfma_ok((int)M, (int)K, (int)gs) != 0, "skinny_i8_sh: unsupported shape (M ", M, ", K ", K,
+              ", gs ", gs, ")");
+  TORCH_CHECK(qsh.numel() == NB * 16 * K && ssh.numel() == NB * 16 * (K / gs), "skinny_i8_sh: qsh / ssh size");
+  TORCH_CHECK(NB * K < ((int64_t)1 << 40) && N < ((int64_t)1 << 31) / 16, "skinny_i8_sh: matrix too large");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(qsh.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_i8_sh: 16-B aligned x / q");
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    need(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kBFloat16, "skinny_i8_sh: bias bf16 [N]");
+    bp = bias->data_ptr();
+  }
+  auto y = torch::empty({M, N}, x.options());
+  auto& ws = i8_workspace(x, N);
+  check(ds_skinny_i8_mfma(x.data_ptr(), qsh.data_ptr<int8_t>(), ssh.data_ptr<float>(), bp, y.data_ptr(),
+                          ws.acc.data_ptr<float>(), (int)M, (int)N, (int)K, (int)gs, stream()),
+        "skinny_i8_sh");
   return y;
 }
 
 void register_inference_ops(pybind11::module& m) {
   m.def("skinny_i8_ok", &skinny_i8_ok);
+  m.def("skinny_i8_sh_ok", &skinny_i8_sh_ok);
+  m.def("skinny_i8_tune", [](int64_t cfg, int64_t wpc, int64_t dbg) { ds_skinny_i8_tune((int)cfg, (int)wpc, (int)dbg); },
+        py::arg("cfg"), py::arg("wpc"), py::arg("dbg") = 0);
   m.def("skinny_i8", &skinny_i8, py::arg("x"), py::arg("q"), py::arg("scales"), py::arg("bias"), py::arg("N"),
-        py::arg("gs"), py::arg("path") = 0);
+        py::arg("gs"));
+  m.def("skinny_i8_sh", &skinny_i8_sh, py::arg("x"), py::arg("qsh"), py::arg("ssh"), py::arg("bias"), py::arg("N"),
+        py::arg("gs"));
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_force_valu", &skinny_force_valu);
   m.def("skinny_set_path", &skinny_set_path);

@@ -1,4 +1,4 @@
-// Weight-only int8 skinny GEMM for decode: y[M, N] = X[M, K] . (Q[N, K] * s[N, K / gs])^T (+ bias), M <= 8.
+// Weight-only int8 skinny GEMM for decode: y[M, N] = X[M, K] . (Q[N, K] * s[N, K / gs])^T (+ bias), M <= 16.
 //
 // Reference counterparts (behaviour, not code): the weight-only int8 inference path of `transformer_inference`
 // (`ds_vector_matmul_int8` / `dequantize_kernel`, `csrc/transformer/inference/csrc/pt_binding.cpp:13xx`,
@@ -6,25 +6,16 @@
 // weight and run a library GEMM.
 //
 // MI355X design: decode GEMMs are pure weight streams, so int8 weights halve the HBM bytes of a bf16 decode step.
-// The dequantisation is fused into the stream: no bf16 copy of the weight is ever written.
-//  * each wave owns 4 consecutive output rows at a time (grid-stride over row quads), each lane a 16-element K chunk
-//    per row per step: one 16-byte non-temporal load per row; the group scale of that chunk (groups of >= 16
-//    elements along K, the quantiser's layout) is one fp32 load;
-//  * UNR chunks are issued before any is consumed (4 rows x UNR x 16 B in flight per lane) to cover HBM latency;
-//  * X (M <= 8 rows) is staged once per workgroup into LDS as bf16 when it fits (<= 64 KB), else read through L2;
-//  * int8 -> f32 by byte extract + convert, fp32 FMA, one wave reduction per (row, token) at the end.
-// That VALU path costs M FMAs per weight byte, so from 4 token rows on the MFMA variant below takes over:
-//  * one workgroup = one 16-row slab of W; its 4 waves split K into quarters; per 64-element K chunk each lane
-//    loads 16 int8 of one row (16 B), turns them into u = q + 128 (sign-bit flip, one v_cvt_f32_ubyte per element,
-//    exact in bf16) and feeds two v_mfma_f32_16x16x32_bf16 with A = u (rows = output features) and B = X^T (cols =
-//    tokens, zero beyond M); two more MFMAs against ones give sum_k x_k, so W.x = s * (u.x - 128 sum x) is applied
-//    per chunk to the accumulator with the row's group scale (no per-element multiply). Both operands use the same
-//    k permutation (lane group g holds k = 16g + j, then 16g + 8 + j), which a sum over k does not see. MFMA
-//    throughput is far above the weight stream, so the cost per byte no longer depends on M (<= 16); the four
-//    quarter sums meet in LDS. Measured ~3 TB/s flat in M (VALU path: 6.1-6.4 TB/s at one row): the lane->row
-//    mapping the MFMA operand dictates gives 64-B row segments per load instruction, which the HBM stream
-//    pays for; staging whole 1-KB row pieces through LDS is the next step.
+// The dequantisation is fused into the stream: no bf16 copy of the weight is ever written. Two kernels:
+//  * VALU stream over a ROW-MAJOR weight (<= 8 rows; kept for callers holding the quantiser's layout): each wave owns
+//    4 consecutive output rows at a time, each lane a 16-element K chunk per row per step (one 16-byte non-temporal
+//    load + one fp32 group scale), UNR chunks in flight, X staged in LDS when it fits, int8 -> f32 by byte extract +
+//    convert, fp32 FMA, one wave reduction per (row, token). Costs M FMAs per weight byte: 6.2 TB/s at one row,
+//    1.5 at eight.
+//  * MFMA stream over the PRE-SHUFFLED weight (ops/int8_gemv.py), the decode path of the inference engine: below.
 #include "ds_hip.h"
+
+#include <algorithm>
 
 namespace {
 
@@ -119,109 +110,257 @@ __global__ void __launch_bounds__(256) skinny_i8_kernel(const bf16* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------------------------- MFMA stream
+// Pre-shuffled weights. The HBM stream wants every load instruction to cover long contiguous segments: measured
+// loads-only (tools/probe_load_patterns.hip, profiles/int8_load_patterns_r2.jsonl) 16 rows x 64 B per instruction
+// (the MFMA operand layout read from a row-major weight: lane & 15 = row) caps at 4.4-5.0 TB/s, 4 rows x 256 B or
+// 1 row x 1 KB reach 6-6.9. Staging a row-major tile through LDS (LDS-DMA, 3-slot ring) fixes the pattern but LDS
+// then bounds the bytes in flight to ~64 KB per CU, which at the loaded HBM latency (~4 us) is 1.5 TB/s (measured).
+// Weights of an inference model are constants, so the quantiser output is re-laid ONCE into operand order instead:
+//   Qsh[nb][kq][lane][16 B] = Q[16 nb + (lane & 15)][64 kq + 16 (lane >> 4) + 0..15]   (1 KB per 16 rows x 64 k)
+//   Ssh[nb][group][16]      = S[16 nb + r][group]
+// so one 16-byte-per-lane load IS the v_mfma_f32_16x16x32_bf16 B operand of two MFMAs (k permuted 16g + j for the
+// first, 16g + 8 + j for the second, X loaded with the same permutation) and each instruction reads 1 KB contiguous.
+//  * a wave owns FB = 4 row blocks (64 output features) and walks a contiguous range of the (block group, k quarter)
+//    sequence; P = 2-3 quarters of weights, X and scales are in flight in registers (compiler-counted vmcnt; the
+//    prologue and every reload are fenced with sched_barrier so hipcc keeps the issue order that makes the counts
+//    static), 12 waves per CU. MORE in flight is slower (measured: 8 waves x 8 KB beat 8 x 32 KB by 1.5x): the
+//    memory pipeline reorders deep per-CU queues into a DRAM-unfriendly stream;
+//  * B = u = q + 128 (byte extract + packed bf16 convert), A = X (token = lane & 15; rows >= M re-read row M-1); two
+//    MFMAs per block for u.x and two per quarter against ones for sum(x), W.x = s * (u.x - 128 sum x) with the
+//    lane's single scale (its accumulator rows are 4 tokens of ONE feature);
+//  * ranges may start / end inside a block group (split-K without a fixed factor, every wave gets the same number
+//    of quarters); partial sums go to a fp32 workspace with f32 atomics and a second small kernel converts it (+ bias)
+//    to bf16 and re-zeroes it: no memset, capturable in a HIP graph. (A last-arriver finalize inside the main kernel
+//    needs device-scope fences, which on the multi-XCD part write back / invalidate the XCD's L2 — measured 3.2 vs
+//    5.4 TB/s for the same loop.)
+// Measured (profiles/int8_skinny_gemv_r2.jsonl, BLOOM-176B shapes 57344x14336 / 14336x57344): 6.3 TB/s at 1 token
+// row, 6.0-6.1 at 8, 5.5-5.9 at 16 (round 1's MFMA kernel: 2.2-3.0; the VALU stream: 6.3 at 1 row, 1.5 at 8).
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-constexpr int MF_UNR = 8;  // 64-element chunks in flight per lane
 
-__global__ void __launch_bounds__(256) skinny_i8_mfma_kernel(const bf16* __restrict__ X, const int8_t* __restrict__ Q,
-                                                             const float* __restrict__ S,
-                                                             const bf16* __restrict__ bias, bf16* __restrict__ Y,
-                                                             int M, int N, int K, int gs) {
-  __shared__ float red[4][16][17];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int g = lane >> 4, l16 = lane & 15;
-  const int n0 = blockIdx.x * 16;
-  const int n = min(n0 + l16, N - 1);       // A row of this lane (clamped; rows >= N are never stored)
-  const int m = l16;                         // B column (token) of this lane
-  const bool xvalid = m < M;
-  const int nchunks = K / 64;
-  const int ngroups = K / gs;
-  const int per = (nchunks + 3) / 4;
-  const int c0 = wid * per, c1 = min(c0 + per, nchunks);
-  const int8_t* qrow = Q + (int64_t)n * K + 16 * g;
-  const bf16* xrow = X + (int64_t)(xvalid ? m : 0) * K + 16 * g;
-  // accumulator rows of this lane are output features 4g + i; their group scales
-  const float* srows[4];
+struct I8Args {
+  const bf16* x;
+  const int8_t* q;   // shuffled
+  const float* s;    // shuffled
+  const bf16* bias;
+  bf16* y;
+  float* acc;  // [16, NP] fp32 workspace, zero between calls
+  int M, N, K, gs, ngroups, NB, KQ, NBG;
+  int qpg;        // k quarters per scale group (gs / 64)
+  int NP;         // workspace row length: NBG * FB * 16
+  int64_t total;  // NBG * KQ
+};
+
+// 16 int8 -> two bf16x8 of u = q + 128 (exact)
+__device__ __forceinline__ void u8x16_to_bf16(const i32x4 wq, bf16x8_t& lo, bf16x8_t& hi) {
+  bf16x8_t o[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) srows[i] = S + (int64_t)min(n0 + 4 * g + i, N - 1) * ngroups;
+  for (int h = 0; h < 2; ++h) {
+    const unsigned a = (unsigned)wq[2 * h] ^ 0x80808080u, b = (unsigned)wq[2 * h + 1] ^ 0x80808080u;
+    f32x4 fa, fb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fa[j] = (float)((a >> (8 * j)) & 0xffu);
+      fb[j] = (float)((b >> (8 * j)) & 0xffu);
+    }
+    const bf16x4 ba = __builtin_convertvector(fa, bf16x4), bb = __builtin_convertvector(fb, bf16x4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[h][j] = ba[j]; o[h][4 + j] = bb[j]; }
+  }
+  lo = o[0];
+  hi = o[1];
+}
+
+template <int FB>
+struct I8Stage {
+  i32x4 w[FB];
+  bf16x8_t x0, x1;
+  float sc[FB];
+};
+
+template <int FB, int P>
+__global__ void __launch_bounds__(256) skinny_i8_mfma_kernel(I8Args a) {
+  const int lane = threadIdx.x & 63;
+  // wave-uniform bookkeeping lives in SGPRs (readfirstlane): scalar branches keep the vmcnt counts static
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)), nw = gridDim.x * 4;
+  const int lo = (int)(a.total * gw / nw), hi = (int)(a.total * (gw + 1) / nw);
+  if (lo >= hi) return;
+  const int r = lane & 15, g = lane >> 4;
+
+  // issue cursor: wave-uniform (SGPR) pointers advanced per quarter; divisions only when entering a block group
+  int ibg = 0, ikq = 0, iql = 0;
+  bool hold = false;
+  int64_t iw = 0, is = 0, ix = 0, fw[FB], fs[FB];
+  const int64_t xlane = (int64_t)min(r, a.M - 1) * a.K + 16 * g + 0;  // token rows >= M re-read row M - 1
+  auto enter = [&](int bgv, int kqv) {
+    if (bgv >= a.NBG) {  // past the end of the range: keep re-loading the last quarter (static vmcnt)
+      bgv = a.NBG - 1;
+      kqv = a.KQ - 1;
+      hold = true;
+    }
+    ibg = bgv;
+    ikq = kqv;
+#pragma unroll
+    for (int f = 0; f < FB; ++f) {
+      const int64_t nb = min(bgv * FB + f, a.NB - 1);
+      fw[f] = nb * a.KQ * 1024;
+      fs[f] = nb * a.ngroups * 16;
+    }
+    iw = (int64_t)kqv * 1024;
+    is = (int64_t)(kqv / a.qpg) * 16;
+    iql = a.qpg - kqv % a.qpg;
+    ix = (int64_t)kqv * 64;
+  };
+  auto advance = [&]() {
+    if (hold) return;
+    if (++ikq == a.KQ) {
+      enter(ibg + 1, 0);
+      return;
+    }
+    iw += 1024;
+    ix += 64;
+    if (--iql == 0) {
+      is += 16;
+      iql = a.qpg;
+    }
+  };
+  auto load = [&](I8Stage<FB>& st) {
+#pragma unroll
+    for (int f = 0; f < FB; ++f)
+      st.w[f] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(a.q + fw[f] + iw + lane * 16));
+#pragma unroll
+    for (int f = 0; f < FB; ++f) st.sc[f] = a.s[fs[f] + is + r];
+    const bf16* xp = a.x + xlane + ix;
+    st.x0 = *reinterpret_cast<const bf16x8_t*>(xp);
+    st.x1 = *reinterpret_cast<const bf16x8_t*>(xp + 8);
+  };
+
   bf16x8_t ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  for (int c = c0; c < c1; c += MF_UNR) {
-    // issue every load of the batch (weights, scales AND the X operand) before any math, so HBM and L2 latency
-    // overlap instead of serialising behind each chunk's MFMAs
-    i32x4 w[MF_UNR];
-    float sc[MF_UNR][4];
-    bf16x8_t b[MF_UNR][2];
+  f32x4 acc[FB];
 #pragma unroll
-    for (int u = 0; u < MF_UNR; ++u) {
-      const int cc = c + u;
-      const bool live = cc < c1;
-      w[u] = live ? __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(qrow + (int64_t)cc * 64))
-                  : i32x4{0, 0, 0, 0};
+  for (int f = 0; f < FB; ++f) acc[f] = zero4;
+
+  int bg = lo / a.KQ, kq = lo - bg * a.KQ;
+  enter(bg, kq);
+  I8Stage<FB> st[P];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sc[u][i] = live ? srows[i][(cc * 64) / gs] : 0.f;
+  for (int p = 0; p < P; ++p) {  // same issue order as the steady state (else vmcnt at the loop head drains all)
+    load(st[p]);
+    advance();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // partial sums of block group `grp` -> fp32 workspace (padded to whole groups; features >= N are never read)
+  auto spill = [&](int grp) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (xvalid && live) {
-          b[u][h] = *reinterpret_cast<const bf16x8_t*>(xrow + (int64_t)cc * 64 + 8 * h);
-        } else {
+    for (int f = 0; f < FB; ++f) {
+      const int n = (grp * FB + f) * 16 + r;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b[u][h][j] = (__bf16)0.f;
-        }
-      }
+      for (int i = 0; i < 4; ++i)
+        if (4 * g + i < a.M) unsafeAtomicAdd(a.acc + (int64_t)(4 * g + i) * a.NP + n, acc[f][i]);
+      acc[f] = zero4;
     }
+  };
+  // Straight-line steady state (no early exit, no fence): hipcc keeps each reload right after the compute that frees
+  // its registers and counts vmcnt statically; steps past the range end compute on re-loaded data with scale 0.
+  for (int base = lo; base < hi; base += P) {
 #pragma unroll
-    for (int u = 0; u < MF_UNR; ++u) {
-      if (c + u >= c1) break;
-      // q (int8) -> u = q + 128 (unsigned byte, exact in bf16) by flipping the sign bits; the -128 offset is
-      // applied to the product afterwards via sum_k x_k (an extra MFMA against ones)
-      bf16x8_t a[2];
+    for (int p = 0; p < P; ++p) {
+      const bool live = base + p < hi;
+      f32x4 px = __builtin_amdgcn_mfma_f32_16x16x32_bf16(st[p].x0, ones, zero4, 0, 0, 0);
+      px = __builtin_amdgcn_mfma_f32_16x16x32_bf16(st[p].x1, ones, px, 0, 0, 0);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const unsigned lo = (unsigned)w[u][2 * h] ^ 0x80808080u, hi = (unsigned)w[u][2 * h + 1] ^ 0x80808080u;
-        f32x4 flo, fhi;
+      for (int f = 0; f < FB; ++f) {
+        bf16x8_t b0, b1;
+        u8x16_to_bf16(st[p].w[f], b0, b1);
+        f32x4 pu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(st[p].x0, b0, zero4, 0, 0, 0);
+        pu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(st[p].x1, b1, pu, 0, 0, 0);
+        const float sc = live ? st[p].sc[f] : 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          flo[j] = (float)((lo >> (8 * j)) & 0xffu);
-          fhi[j] = (float)((hi >> (8 * j)) & 0xffu);
-        }
-        const bf16x4 blo = __builtin_convertvector(flo, bf16x4), bhi = __builtin_convertvector(fhi, bf16x4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { a[h][j] = blo[j]; a[h][4 + j] = bhi[j]; }
+        for (int i = 0; i < 4; ++i) acc[f][i] = fmaf(sc, fmaf(-128.f, px[i], pu[i]), acc[f][i]);
       }
-      f32x4 pu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[u][0], zero4, 0, 0, 0);
-      pu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[u][1], pu, 0, 0, 0);
-      f32x4 px = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, b[u][0], zero4, 0, 0, 0);
-      px = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, b[u][1], px, 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = fmaf(sc[u][i], fmaf(-128.f, px[i], pu[i]), acc[i]);
+      if (live && kq == a.KQ - 1) spill(bg);
+      if (++kq == a.KQ) { kq = 0; ++bg; }
+      __builtin_amdgcn_sched_barrier(0);
+      load(st[p]);
+      advance();
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
-  // C: col = token (lane & 15), rows = output features 4g + i
-#pragma unroll
-  for (int i = 0; i < 4; ++i) red[wid][4 * g + i][l16] = acc[i];
-  __syncthreads();
-  const int row = tid >> 4, tok = tid & 15;
-  if (tok < M && n0 + row < N) {
-    const float v = red[0][row][tok] + red[1][row][tok] + red[2][row][tok] + red[3][row][tok];
-    Y[(int64_t)tok * N + n0 + row] = (bf16)(v + (bias ? (float)bias[n0 + row] : 0.f));
-  }
+  if ((hi % a.KQ) != 0) spill((hi - 1) / a.KQ);  // the range ends inside a group
+}
+
+// y = bf16(workspace + bias) for the M token rows; the workspace is re-zeroed over everything the spills touched
+// (rows < M, all NP padded columns), so the next call — whatever its N — starts from 0.
+__global__ void __launch_bounds__(256) skinny_i8_finalize(float* __restrict__ acc, const bf16* __restrict__ bias,
+                                                          bf16* __restrict__ y, int M, int N, int NP) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)M * NP) return;
+  const int t = (int)(e / NP), n = (int)(e % NP);
+  const float v = acc[e];
+  acc[e] = 0.f;
+  if (n < N) y[(int64_t)t * N + n] = (bf16)(v + (bias ? (float)bias[n] : 0.f));
 }
 
 }  // namespace
+
+// Variant override for tools/sweep_int8_gemv.py (0 = measured default below): (FB, P) kernel and resident waves / CU.
+static int g_i8_cfg = 0, g_i8_wpc = 0;
+extern "C" void ds_skinny_i8_tune(int cfg, int wpc, int) {
+  g_i8_cfg = cfg;
+  g_i8_wpc = wpc;
+}
 
 extern "C" int ds_skinny_i8_mfma_ok(int M, int K, int gs) {
   return M >= 1 && M <= 16 && K % 64 == 0 && gs % 64 == 0 && K % gs == 0;
 }
 
-// same contract as ds_skinny_i8 for M <= 16 token rows (K % 64 == 0, group size a multiple of 64)
-extern "C" int ds_skinny_i8_mfma(const void* X, const int8_t* Q, const float* S, const void* bias, void* Y, int M,
-                                 int N, int K, int gs, hipStream_t st) {
+// workspace the caller keeps per stream: fp32 [16 rows x N padded to whole block groups], zero-filled once
+extern "C" int64_t ds_skinny_i8_mfma_ws_floats(int N) { return 16LL * (((N + 15) / 16 + 3) / 4) * 64; }
+
+// X [M, K] bf16 (M <= 16), Qsh / Ssh in the shuffled layout above (N padded to a multiple of 16), bias bf16 [N] or
+// null -> Y [M, N] bf16
+extern "C" int ds_skinny_i8_mfma(const void* X, const int8_t* Qsh, const float* Ssh, const void* bias, void* Y,
+                                 float* ws, int M, int N, int K, int gs, hipStream_t st) {
   if (!ds_skinny_i8_mfma_ok(M, K, gs) || N <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(skinny_i8_mfma_kernel, dim3((N + 15) / 16), dim3(256), 0, st, (const bf16*)X, Q, S,
-                     (const bf16*)bias, (bf16*)Y, M, N, K, gs);
+  I8Args a;
+  a.x = (const bf16*)X;
+  a.q = Qsh;
+  a.s = Ssh;
+  a.bias = (const bf16*)bias;
+  a.y = (bf16*)Y;
+  a.acc = ws;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.gs = gs;
+  a.ngroups = K / gs;
+  a.qpg = gs / 64;
+  a.NB = (N + 15) / 16;
+  a.KQ = K / 64;
+  auto go = [&](auto kern, int P, int FB, int wpc) {
+    // one resident round of waves (wpc per CU, from the VGPR budget), each with the same number of quarters
+    const int nbg = (a.NB + FB - 1) / FB;
+    a.NBG = nbg;
+    a.NP = nbg * FB * 16;
+    a.total = (int64_t)nbg * a.KQ;
+    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(a.total / (2 * P), 256 * wpc));
+    hipLaunchKernelGGL(kern, dim3((int)((waves + 3) / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(skinny_i8_finalize, dim3((int)(((int64_t)M * a.NP + 255) / 256)), dim3(256), 0, st, ws,
+                       (const bf16*)bias, (bf16*)Y, M, N, a.NP);
+  };
+  // measured (tools/sweep_int8_gemv.py, profiles/int8_skinny_gemv_r2.jsonl): FB 4 / P 2 at 12 waves per CU (128
+  // registers) up to 8 token rows, FB 4 / P 3 at 8 waves per CU above (more MFMA work per byte wants fewer waves)
+  int cfg = g_i8_cfg ? g_i8_cfg : (M > 8 ? 2 : 1);
+  const int wpc = g_i8_wpc;
+  switch (cfg) {
+    case 2: go(skinny_i8_mfma_kernel<4, 3>, 3, 4, wpc ? wpc : 8); break;
+    case 3: go(skinny_i8_mfma_kernel<4, 4>, 4, 4, wpc ? wpc : 8); break;
+    case 4: go(skinny_i8_mfma_kernel<2, 2>, 2, 2, wpc ? wpc : 16); break;
+    default: go(skinny_i8_mfma_kernel<4, 2>, 2, 4, wpc ? wpc : 12);
+  }
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,86 @@
+"""Weight-only int8 linear layers for decode: group-quantised weights stored once in MFMA operand order.
+
+Reference counterparts (behaviour): the weight-only int8 inference path of `transformer_inference`
+(`csrc/transformer/inference/csrc/pt_binding.cpp` `ds_vector_matmul_int8` + `dequantize.cu:15-86`) and v2's
+`mixed_gemm` (CUTLASS). Both dequantise (or stream-dequantise) a row-major weight into a library GEMM.
+
+MI355X design (`csrc/gemv/skinny_int8.hip`): a decode GEMM is a weight stream, and the HBM stream only runs at full
+rate when each 16-byte-per-lane load covers long contiguous segments — which the MFMA operand layout read from a
+row-major matrix does not (measured 4.4-5 TB/s loads-only). Inference weights are constants, so the int8 matrix is
+re-laid ONCE at quantisation time:
+
+    qsh[nb, kq, lane, :] = q[16 nb + (lane % 16), 64 kq + 16 (lane // 16) : +16]     (int8, 1 KB per 16 x 64 tile)
+    ssh[nb, group, r]    = scales[16 nb + r, group]
+
+so one contiguous 1 KB load per wave is exactly the B operand of two v_mfma_f32_16x16x32_bf16. Prefill (more than 16
+token rows) un-shuffles with a view/permute and dequantises into a bf16 temporary for the library GEMM.
+"""
+import torch
+import torch.nn.functional as F
+
+from .native import hip_ops
+from .quantizer import QuantizedTensor, dequantize, quantize
+
+MAX_DECODE_ROWS = 16
+
+
+def preshuffle(q, scales, group_size):
+    """Row-major int8 q [N, K] + fp32 scales [N * K / gs] -> (qsh [NB, K/64, 64, 16], ssh [NB, K/gs, 16]), N padded
+    to NB * 16 rows with zero weights / zero scales."""
+    N, K = q.shape
+    if K % 64 or group_size % 64 or K % group_size:
+        raise ValueError(f"preshuffle needs K and group size multiples of 64 (K={K}, gs={group_size})")
+    nb = (N + 15) // 16
+    s = scales.reshape(N, K // group_size)
+    if nb * 16 != N:
+        q = F.pad(q, (0, 0, 0, nb * 16 - N))
+        s = F.pad(s, (0, 0, 0, nb * 16 - N))
+    qsh = q.reshape(nb, 16, K // 64, 4, 16).permute(0, 2, 3, 1, 4).reshape(nb, K // 64, 64, 16).contiguous()
+    ssh = s.reshape(nb, 16, K // group_size).permute(0, 2, 1).contiguous()
+    return qsh, ssh
+
+
+def unshuffle(qsh, ssh, N):
+    """Inverse of `preshuffle`: (q [N, K] int8, scales [N * K / gs] fp32)."""
+    nb, kq = qsh.shape[0], qsh.shape[1]
+    q = qsh.reshape(nb, kq, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(nb * 16, kq * 64)[:N]
+    s = ssh.permute(0, 2, 1).reshape(nb * 16, ssh.shape[1])[:N]
+    return q.contiguous(), s.reshape(-1).contiguous()
+
+
+class Int8Weight:
+    """Symmetric group-quantised weight [N, K] kept in the pre-shuffled layout."""
+
+    def __init__(self, w, group_size=64):
+        N, K = w.shape
+        self.shape = w.shape
+        self.dtype = w.dtype
+        self.group_size = min(group_size, K)
+        qt = quantize(w.contiguous(), group_size=self.group_size, bits=8, symmetric=True)
+        self.qsh, self.ssh = preshuffle(qt.data.view(N, K), qt.scales, self.group_size)
+
+    @staticmethod
+    def supported(w, bits=8, group_size=64):
+        return bits == 8 and w.dim() == 2 and w.shape[1] % 64 == 0 and min(group_size, w.shape[1]) % 64 == 0 \
+            and w.shape[1] % min(group_size, w.shape[1]) == 0
+
+    def nbytes(self):
+        return self.qsh.numel() + self.ssh.numel() * 4
+
+    def materialize(self, dtype=None):
+        q, s = unshuffle(self.qsh, self.ssh, self.shape[0])
+        qt = QuantizedTensor(q.reshape(-1), s, torch.empty(0, device=q.device), self.shape, self.group_size, 8,
+                             self.dtype)
+        return dequantize(qt, dtype or self.dtype)
+
+    def linear(self, x, bias=None):
+        """x [..., K] -> x . W^T (+ bias). Up to 16 token rows on a GPU: the fused MFMA stream (no bf16 weight is
+        ever written); otherwise dequantise + library GEMM."""
+        K = x.shape[-1]
+        M = x.numel() // K
+        if x.is_cuda and x.dtype == torch.bfloat16 and M <= MAX_DECODE_ROWS and \
+                (bias is None or bias.dtype == torch.bfloat16):
+            y = hip_ops().skinny_i8_sh(x.reshape(M, K).contiguous(), self.qsh, self.ssh, bias, self.shape[0],
+                                       self.group_size)
+            return y.view(*x.shape[:-1], self.shape[0])
+        return F.linear(x, self.materialize(x.dtype), bias)

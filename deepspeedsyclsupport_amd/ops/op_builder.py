@@ -47,8 +47,10 @@ EXTENSIONS = {
             "gemv/skinny_mfma.hip",
             "gemv/skinny_int8.hip",
             "moe/moe_kernels.hip",
+            "comm/xgmi_allreduce.hip",
         ],
-        "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp", "bind/moe_bind.cpp", "bind/host_mem.cpp"],
+        "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp", "bind/moe_bind.cpp", "bind/host_mem.cpp",
+                     "bind/comm_bind.cpp"],
     },
     # host ops: CPU Adam/Adagrad/Lion (ZeRO-Offload, Twin-Flow), async tensor I/O (ZeRO-Infinity), shm all-reduce
     "ds_cpu_ops": {

@@ -514,24 +514,65 @@ def test_spatial_nhwc_bias_add(dt):
 
 
 @pytest.mark.parametrize("M", [1, 2, 4, 5, 8, 16])
-@pytest.mark.parametrize("N,K,gs", [(1, 64, 64), (13, 4096, 64), (4096, 11008, 64), (1000, 14336, 128), (300, 57344, 64)])
+@pytest.mark.parametrize("N,K,gs", [(1, 64, 64), (13, 4096, 64), (4096, 11008, 64), (1000, 14336, 128), (300, 57344, 64),
+                                    (77, 320, 64), (50, 4160, 64), (129, 2048, 512), (64, 1024, 1024)])
 @pytest.mark.parametrize("bias", [False, True])
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", ["valu", "mfma"])
 def test_skinny_int8_gemv(M, N, K, gs, bias, path):
-    """Weight-only int8 decode GEMV (fused group dequant) vs an fp32 GEMM on the dequantised weight."""
+    """Weight-only int8 decode GEMV (fused group dequant) vs an fp32 GEMM on the dequantised weight: the VALU stream
+    over the row-major weight (<= 8 rows) and the MFMA stream over the pre-shuffled weight (<= 16 rows)."""
+    from deepspeedsyclsupport_amd.ops.int8_gemv import preshuffle
     from deepspeedsyclsupport_amd.ops.quantizer import dequantize, quantize
     torch.manual_seed(N + K)
     w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
     qt = quantize(w, group_size=gs, bits=8, symmetric=True)
     x = torch.randn(M, K, device="cuda").bfloat16()
     b = torch.randn(N, device="cuda").bfloat16() if bias else None
-    if (path == 1 and M > 8) or (path == 2 and K % 64):
-        pytest.skip("shape outside this path")
-    y = ops().skinny_i8(x, qt.data, qt.scales, b, N, gs, path)
+    if path == "valu":
+        if M > 8:
+            pytest.skip("VALU stream is for <= 8 rows")
+        y = ops().skinny_i8(x, qt.data, qt.scales, b, N, gs)
+    else:
+        qsh, ssh = preshuffle(qt.data.view(N, K), qt.scales, gs)
+        y = ops().skinny_i8_sh(x, qsh, ssh, b, N, gs)
     ref = x.float() @ dequantize(qt, torch.float32).t()
     if bias:
         ref = ref + b.float()
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * max(1.0, ref.abs().max().item()))
+
+
+def test_skinny_int8_mfma_workspace_reuse_and_graph():
+    """The MFMA path's split-K workspace re-zeroes itself: repeated calls, interleaved shapes and a HIP-graph replay
+    all give the first call's result; Int8Weight.linear routes decode sizes to it and prefill to dequant + GEMM."""
+    from deepspeedsyclsupport_amd.ops.int8_gemv import Int8Weight
+    torch.manual_seed(3)
+    mats = []
+    for N, K in ((4096, 4096), (11008, 4096), (333, 8192)):
+        wt = Int8Weight((torch.randn(N, K, device="cuda") * 0.02).bfloat16(), 64)
+        mats.append((wt, torch.randn(8, K, device="cuda").bfloat16()))
+    first = [wt.linear(x) for wt, x in mats]
+    for wt, x in mats:
+        ref = x.float() @ wt.materialize(torch.float32).t()
+        torch.testing.assert_close(first[mats.index((wt, x))].float(), ref, rtol=2e-2, atol=2e-2)
+    for _ in range(3):
+        for (wt, x), y0 in zip(mats, first):
+            torch.testing.assert_close(wt.linear(x), y0, rtol=1e-2, atol=1e-2)
+    wt, x = mats[1]
+    xp = torch.randn(40, x.shape[1], device="cuda").bfloat16()  # prefill-sized: dequant + library GEMM
+    torch.testing.assert_close(wt.linear(xp).float(), xp.float() @ wt.materialize(torch.float32).t(), rtol=2e-2,
+                               atol=2e-2)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        wt.linear(x)  # workspace for this stream exists before capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        yg = wt.linear(x)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(yg, first[1], rtol=1e-2, atol=1e-2)
 
 
 @pytest.mark.parametrize("H", [14336, 16384])

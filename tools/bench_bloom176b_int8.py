@@ -79,7 +79,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     model, spec = build(args.layers, dev)
-    n_q = sum(layer.quant[n].qt.data.numel() for layer in model.layers for n in layer.quant)
+    n_q = sum(layer.quant[n].i8.qsh.numel() if layer.quant[n].i8 is not None else layer.quant[n].qt.data.numel()
+              for layer in model.layers for n in layer.quant)
     weights_gib = torch.cuda.memory_allocated() / 2**30
     log(f"[bloom] built: {n_q / 1e9:.1f}B int8 layer params + embedding, {weights_gib:.1f} GiB on device")
     cfg = DeepSpeedInferenceConfig(dtype="bf16", enable_cuda_graph=bool(args.graph), max_tokens=args.prompt + args.gen)

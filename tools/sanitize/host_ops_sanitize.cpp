@@ -78,17 +78,19 @@ static void run_aio(const std::string& dir) {
 }
 
 static int shm_rank(const std::string& name, int rank) {
-  shm_init(name, rank, 2, 1 << 20);
+  const int64_t h = shm_init(name, rank, 2, 1 << 20);
+  shm_barrier(h);
+  if (rank == 0) shm_release_name(h);
   for (int it = 0; it < 3; ++it) {
     auto t = torch::full({100003}, (float)(rank + 1 + it));
-    shm_allreduce(t);
+    shm_allreduce(h, t);
     if (!torch::allclose(t, torch::full({100003}, (float)(3 + 2 * it)))) return 4;
     auto tb = torch::full({4099}, (float)(rank + 1), torch::TensorOptions().dtype(at::kBFloat16));
-    shm_allreduce(tb);
+    shm_allreduce(h, tb);
     if (!torch::allclose(tb.to(at::kFloat), torch::full({4099}, 3.f))) return 5;
-    shm_barrier();
+    shm_barrier(h);
   }
-  shm_finalize();
+  shm_finalize(h);
   return 0;
 }
 

@@ -1,9 +1,6 @@
 #!/usr/bin/env python3
-"""Int8 weight-only skinny GEMM paths (VALU stream over the row-major weight vs MFMA over the pre-shuffled one) at BLOOM-176B / Llama shapes: effective weight TB/s.
-
-    python tools/bench_int8_gemv.py [quick]
-Bytes counted: int8 weights + fp32 group scales (gs 64), the HBM stream the op must read.
-"""
+"""Interleaved sweep of the int8 MFMA GEMV variants in ONE process (box-to-box variance is large, so variants are
+compared side by side): `python tools/sweep_int8_gemv.py cfg:wpc[:dbg] ...`."""
 import json
 import os
 import sys
@@ -28,21 +25,22 @@ def timeit(fn, iters=20):
     return (time.perf_counter() - t) / iters
 
 
-quick = "quick" in sys.argv[1:]
-shapes = ((57344, 14336), (14336, 57344), (43008, 14336), (11008 * 2, 4096), (4096, 4096))
-for N, K in shapes[:2] if quick else shapes:
+variants = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:]] or [(0, 8)]
+for N, K in ((57344, 14336), (14336, 57344), (22016, 4096)):
     w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
     qt = quantize(w, group_size=64, bits=8)
     del w
     qsh, ssh = preshuffle(qt.data.view(N, K), qt.scales, 64)
-    for M in (1, 2, 4, 8, 16):
+    nbytes = N * K * (1 + 4 / 64)
+    for M in (1, 8, 16):
         x = torch.randn(M, K, device="cuda").bfloat16()
         row = {"N": N, "K": K, "M": M}
-        for name, fn in (("valu", lambda: hip_ops().skinny_i8(x, qt.data, qt.scales, None, N, 64)),
-                         ("mfma", lambda: hip_ops().skinny_i8_sh(x, qsh, ssh, None, N, 64))):
-            if name == "valu" and M > 8:
-                continue
-            t = timeit(fn)
-            row[f"{name}_us"] = round(t * 1e6, 1)
-            row[f"{name}_tb_s"] = round((N * K * (1 + 4 / 64)) / t / 1e12, 2)
+        if M <= 8:
+            row["valu"] = round(nbytes / timeit(lambda: hip_ops().skinny_i8(x, qt.data, qt.scales, None, N, 64)) / 1e12, 2)
+        for rep in range(2):
+            for v in variants:
+                hip_ops().skinny_i8_tune(v[0], v[1], v[2] if len(v) > 2 else 0)
+                t = timeit(lambda: hip_ops().skinny_i8_sh(x, qsh, ssh, None, N, 64))
+                key = ":".join(map(str, v))
+                row[key] = max(row.get(key, 0), round(nbytes / t / 1e12, 2))
         print(json.dumps(row), flush=True)
