@@ -29,6 +29,7 @@ int ds_skinny_i8_mfma(const void*, const int8_t*, const float*, const void*, voi
                       hipStream_t);
 int64_t ds_skinny_i8_mfma_ws_floats(int);
 void ds_skinny_i8_tune(int, int, int);
+int ds_dequant_sh(const int8_t*, const float*, void*, int, int, int, hipStream_t);
 int ds_skinny_i8(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
 int ds_quantize(const void*, int8_t*, float*, float*, int64_t, int, int, int, int, unsigned, int, hipStream_t);
 int ds_dequantize(const int8_t*, const float*, const float*, void*, int64_t, int, int, int, int, hipStream_t);
@@ -296,7 +297,20 @@ Tensor skinny_i8_sh(Tensor x, Tensor qsh, Tensor ssh, OptT bias, int64_t N, int6
   return y;
 }
 
+// pre-shuffled int8 (ops/int8_gemv.py) -> row-major bf16 [N, K]
+Tensor dequant_sh(Tensor qsh, Tensor ssh, int64_t N, int64_t gs) {
+  need(qsh, "qsh"); need(ssh, "ssh");
+  TORCH_CHECK(qsh.scalar_type() == at::kChar && ssh.scalar_type() == at::kFloat && qsh.dim() == 4, "dequant_sh: layout");
+  const int64_t K = qsh.size(1) * 64;
+  TORCH_CHECK(qsh.size(0) == (N + 15) / 16 && ssh.numel() == qsh.size(0) * 16 * (K / gs), "dequant_sh: sizes");
+  auto w = torch::empty({N, K}, qsh.options().dtype(at::kBFloat16));
+  check(ds_dequant_sh(qsh.data_ptr<int8_t>(), ssh.data_ptr<float>(), w.data_ptr(), (int)N, (int)K, (int)gs, stream()),
+        "dequant_sh");
+  return w;
+}
+
 void register_inference_ops(pybind11::module& m) {
+  m.def("dequant_sh", &dequant_sh);
   m.def("skinny_i8_ok", &skinny_i8_ok);
   m.def("skinny_i8_sh_ok", &skinny_i8_sh_ok);
   m.def("skinny_i8_tune", [](int64_t cfg, int64_t wpc, int64_t dbg) { ds_skinny_i8_tune((int)cfg, (int)wpc, (int)dbg); },

@@ -304,7 +304,39 @@ __global__ void __launch_bounds__(256) skinny_i8_finalize(float* __restrict__ ac
   if (n < N) y[(int64_t)t * N + n] = (bf16)(v + (bias ? (float)bias[n] : 0.f));
 }
 
+// Pre-shuffled int8 -> row-major bf16 [N, K] (prefill: the library GEMM wants the plain matrix). One thread per
+// 16-byte lane chunk: 16 weights of one row, one scale, 32 contiguous output bytes.
+__global__ void __launch_bounds__(256) dequant_sh_kernel(const int8_t* __restrict__ Qsh, const float* __restrict__ Ssh,
+                                                         bf16* __restrict__ W, int N, int KQ, int ngroups, int qpg) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;  // chunk index = (nb * KQ + kq) * 64 + lane
+  const int lane = (int)(c & 63);
+  const int64_t t = c >> 6;
+  const int kq = (int)(t % KQ), nb = (int)(t / KQ);
+  const int row = nb * 16 + (lane & 15);
+  if (row >= N) return;
+  const float sc = Ssh[((int64_t)nb * ngroups + kq / qpg) * 16 + (lane & 15)];
+  const i32x4 q = *reinterpret_cast<const i32x4*>(Qsh + c * 16);
+  bf16x8 o[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[h][j] = (bf16)(sc * (float)(int8_t)((q[2 * h + j / 4] >> (8 * (j & 3))) & 0xff));
+  bf16* dst = W + (int64_t)row * KQ * 64 + kq * 64 + 16 * (lane >> 4);
+  *reinterpret_cast<bf16x8*>(dst) = o[0];
+  *reinterpret_cast<bf16x8*>(dst + 8) = o[1];
+}
+
 }  // namespace
+
+extern "C" int ds_dequant_sh(const int8_t* Qsh, const float* Ssh, void* W, int N, int K, int gs, hipStream_t st) {
+  if (N <= 0 || K % 64 || gs % 64 || K % gs) return (int)hipErrorInvalidValue;
+  const int KQ = K / 64, NB = (N + 15) / 16;
+  const int64_t chunks = (int64_t)NB * KQ * 64;
+  hipLaunchKernelGGL(dequant_sh_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st, Qsh, Ssh, (bf16*)W,
+                     N, KQ, K / gs, gs / 64);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
 
 // Variant override for tools/sweep_int8_gemv.py (0 = measured default below): (FB, P) kernel and resident waves / CU.
 static int g_i8_cfg = 0, g_i8_wpc = 0;

@@ -13,7 +13,8 @@ re-laid ONCE at quantisation time:
     ssh[nb, group, r]    = scales[16 nb + r, group]
 
 so one contiguous 1 KB load per wave is exactly the B operand of two v_mfma_f32_16x16x32_bf16. Prefill (more than 16
-token rows) un-shuffles with a view/permute and dequantises into a bf16 temporary for the library GEMM.
+token rows) dequantises straight from the shuffled layout into a row-major bf16 temporary (`dequant_sh`) for the
+library GEMM.
 """
 import torch
 import torch.nn.functional as F
@@ -68,10 +69,13 @@ class Int8Weight:
         return self.qsh.numel() + self.ssh.numel() * 4
 
     def materialize(self, dtype=None):
+        dtype = dtype or self.dtype
+        if self.qsh.is_cuda and dtype == torch.bfloat16:
+            return hip_ops().dequant_sh(self.qsh, self.ssh, self.shape[0], self.group_size)
         q, s = unshuffle(self.qsh, self.ssh, self.shape[0])
         qt = QuantizedTensor(q.reshape(-1), s, torch.empty(0, device=q.device), self.shape, self.group_size, 8,
                              self.dtype)
-        return dequantize(qt, dtype or self.dtype)
+        return dequantize(qt, dtype)
 
     def linear(self, x, bias=None):
         """x [..., K] -> x . W^T (+ bias). Up to 16 token rows on a GPU: the fused MFMA stream (no bf16 weight is

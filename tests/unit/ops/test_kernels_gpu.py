@@ -551,6 +551,8 @@ def test_skinny_int8_mfma_workspace_reuse_and_graph():
         wt = Int8Weight((torch.randn(N, K, device="cuda") * 0.02).bfloat16(), 64)
         mats.append((wt, torch.randn(8, K, device="cuda").bfloat16()))
     first = [wt.linear(x) for wt, x in mats]
+    for wt, x in mats:  # native bf16 dequant from the shuffled layout == host un-shuffle + dequant
+        torch.testing.assert_close(wt.materialize().float(), wt.materialize(torch.float32), rtol=1e-2, atol=1e-4)
     for wt, x in mats:
         ref = x.float() @ wt.materialize(torch.float32).t()
         torch.testing.assert_close(first[mats.index((wt, x))].float(), ref, rtol=2e-2, atol=2e-2)
