@@ -123,6 +123,58 @@ class BatchMeta:
     prefill_from_zero: bool          # every sequence starts at position 0 (pure prefill)
 
 
+@dataclass
+class RaggedMeta:
+    """One ragged batch (inference v2 `put()`): the new tokens of every sequence concatenated, decode sequences (one
+    token each) first, then prompt / chunk sequences. Device tensors come from ONE packed host->device copy
+    (`RaggedMeta.build`); the host lists are kept so no step needs a device->host sync."""
+    block_tables: torch.Tensor       # [S, max_blocks] int32
+    start_pos: torch.Tensor          # [S] tokens cached before this step
+    seq_lens: torch.Tensor           # [S] start + new
+    pos_ids: torch.Tensor            # [T] absolute position (= cache slot) of every token
+    seq_ids: torch.Tensor            # [T] sequence of every token
+    cu_q: torch.Tensor               # [S + 1] token offsets
+    work: torch.Tensor               # [W, 2] (sequence, 128-row query block) for the prefill sequences
+    last_idx: torch.Tensor           # [S] row of each sequence's last token
+    n_decode: int                    # sequences [0, n_decode) are single-token decodes
+    cu_host: List[int]
+    start_host: List[int]
+    max_len: int                     # host upper bound of seq_lens (decode split sizing)
+    block_size: int
+
+    @staticmethod
+    def build(starts, n_new, block_lists, n_decode, block_size, device):
+        S = len(starts)
+        cu = [0]
+        for n in n_new:
+            cu.append(cu[-1] + n)
+        T = cu[-1]
+        width = max(1, max(len(b) for b in block_lists))
+        pos, sid = [], []
+        for i, (st, n) in enumerate(zip(starts, n_new)):
+            pos.extend(range(st, st + n))
+            sid.extend([i] * n)
+        work = [(i, qb) for i in range(n_decode, S) for qb in range(-(-n_new[i] // 128))]
+        bt = []
+        for b in block_lists:
+            bt.extend(list(b) + [0] * (width - len(b)))
+        lens = [st + n for st, n in zip(starts, n_new)]
+        last = [c - 1 for c in cu[1:]]
+        flat = pos + sid + list(starts) + lens + cu + [x for w in work for x in w] + last + bt
+        buf = torch.tensor(flat, dtype=torch.int32)
+        if device is not None and torch.device(device).type == "cuda":
+            buf = buf.pin_memory().to(device, non_blocking=True)
+        views, o = [], 0
+        for n in (T, T, S, S, S + 1, 2 * len(work), S, S * width):
+            views.append(buf[o:o + n])
+            o += n
+        pos_t, sid_t, st_t, len_t, cu_t, work_t, last_t, bt_t = views
+        return RaggedMeta(block_tables=bt_t.view(S, width), start_pos=st_t, seq_lens=len_t, pos_ids=pos_t,
+                          seq_ids=sid_t, cu_q=cu_t, work=work_t.view(-1, 2), last_idx=last_t.long(),
+                          n_decode=n_decode, cu_host=cu, start_host=list(starts), max_len=width * block_size,
+                          block_size=block_size)
+
+
 class DSInferenceLayer(nn.Module):
 
     def __init__(self, spec: DSModelSpec, layer_idx: int, tp_group=None, tp_size=1, dtype=torch.bfloat16,
@@ -195,15 +247,22 @@ class DSInferenceLayer(nn.Module):
     # ------------------------------------------------------------------------------------------ attention
     def _attend(self, qkv, meta: BatchMeta, cache, rope, alibi):
         """qkv [B, n, (Hq+2Hk)*D] -> attention output [B, n, Hq*D] (RoPE + cache append + prefill/decode attention)."""
+        if isinstance(meta, RaggedMeta):
+            return self._attend_ragged(qkv, meta, cache, rope, alibi)
         spec = self.spec
         B, n, D = qkv.shape[0], meta.n_new, spec.head_dim
         kc, vc = cache.k[self.layer_idx], cache.v[self.layer_idx]
         k = v = None
+        scale = spec.attn_scale or 1.0 / math.sqrt(D)
+        window = spec.layer_windows[self.layer_idx] if spec.layer_windows else spec.sliding_window
+        # ALiBi / windowed prompts and chunk continuations: ragged paged flash prefill over the cache
+        paged = n > 1 and D == 128 and qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16 \
+            and (not meta.prefill_from_zero or alibi is not None or bool(window))
         if qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16:
             # one fused HIP epilogue: split + RoPE(q, k) + scatter k/v into the paged cache
             from ...ops.native import hip_ops
             rot = spec.rotary_dim if spec.pos in ("rope", "rope_gptj") else 0
-            want_kv = meta.prefill_from_zero and n > 1
+            want_kv = meta.prefill_from_zero and n > 1 and not paged
             outs = hip_ops().qkv_rope_append(qkv.contiguous(), rope[0] if rot else None, rope[1] if rot else None,
                                              meta.pos_ids, kc, vc, meta.block_tables, meta.start_pos, n, self.hq,
                                              self.hk, rot, spec.pos == "rope_gptj", want_kv)
@@ -221,15 +280,42 @@ class DSInferenceLayer(nn.Module):
                 DF.apply_rotary_pos_emb(k, rope[0], rope[1], position_ids=pos, rotary_dim=spec.rotary_dim,
                                         interleaved=inter)
             _kv_append(k, v, kc, vc, meta)
-        scale = spec.attn_scale or 1.0 / math.sqrt(D)
-        window = spec.layer_windows[self.layer_idx] if spec.layer_windows else spec.sliding_window
-        if meta.prefill_from_zero and n > 1:
-            o = _prefill_attention(q, k, v, scale, alibi, window)
-        elif n == 1:
+        if n == 1:
             o = _decode_attention(q.view(B, self.hq, D), kc, vc, meta, scale, alibi, window)
+        elif paged:
+            o = _paged_attention_uniform(q, kc, vc, meta, scale, alibi, window)
+        elif meta.prefill_from_zero:
+            o = _prefill_attention(q, k, v, scale, alibi, window)
         else:
             o = _cached_attention(q, kc, vc, meta, scale, alibi, window)
         return o.reshape(B, n, self.hq * D)
+
+    def _attend_ragged(self, qkv, meta: "RaggedMeta", cache, rope, alibi):
+        """Ragged batch: qkv [1, T, (Hq+2Hk)*D] -> [1, T, Hq*D]. One fused epilogue (RoPE + paged-cache append) for
+        all tokens, then the paged decode kernel for the leading single-token sequences and the ragged paged
+        flash-prefill kernel for the prompt / chunk sequences (`csrc/attn/paged_prefill.hip`)."""
+        spec = self.spec
+        T, D = meta.cu_host[-1], spec.head_dim
+        kc, vc = cache.k[self.layer_idx], cache.v[self.layer_idx]
+        rot = spec.rotary_dim if spec.pos in ("rope", "rope_gptj") else 0
+        inter = spec.pos == "rope_gptj"
+        if qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16:
+            from ...ops.native import hip_ops
+            q = hip_ops().qkv_rope_append(qkv.reshape(T, -1).contiguous(), rope[0] if rot else None,
+                                          rope[1] if rot else None, meta.pos_ids, kc, vc, meta.block_tables,
+                                          meta.start_pos, 1, self.hq, self.hk, rot, inter, False, meta.seq_ids)[0]
+        else:
+            q, k, v = qkv.reshape(1, T, self.hq + 2 * self.hk, D).split([self.hq, self.hk, self.hk], dim=2)
+            q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+            if rot:
+                pos = meta.pos_ids.view(1, T)
+                DF.apply_rotary_pos_emb(q, rope[0], rope[1], position_ids=pos, rotary_dim=rot, interleaved=inter)
+                DF.apply_rotary_pos_emb(k, rope[0], rope[1], position_ids=pos, rotary_dim=rot, interleaved=inter)
+            _kv_append_ragged(k[0], v[0], kc, vc, meta)
+            q = q[0]
+        scale = spec.attn_scale or 1.0 / math.sqrt(D)
+        window = spec.layer_windows[self.layer_idx] if spec.layer_windows else spec.sliding_window
+        return _ragged_attention(q, kc, vc, meta, scale, alibi, window).reshape(1, T, self.hq * D)
 
     def _attention(self, x, meta: BatchMeta, cache, rope, alibi):
         qkv = self._linear(x, "qkv_w", self.qkv_b)
@@ -404,6 +490,79 @@ def _cached_attention(q, kc, vc, meta, scale, alibi, window):
     return torch.stack(outs, 0)
 
 
+def _paged_attention_uniform(q, kc, vc, meta, scale, alibi, window):
+    """Uniform batch (v1 engine): q [B, n, Hq, 128] at positions start..start+n-1 per sequence -> [B, n, Hq, 128]
+    through the ragged paged flash-prefill kernel (K/V of the new tokens are already in the cache)."""
+    from ...ops.native import hip_ops
+    B, n, Hq, D = q.shape
+    cu = torch.arange(0, (B + 1) * n, n, dtype=torch.int32, device=q.device)
+    work = torch.tensor([(b, qb) for b in range(B) for qb in range(-(-n // 128))], dtype=torch.int32).to(
+        q.device, non_blocking=True)
+    o = hip_ops().paged_prefill(q.reshape(B * n, Hq, D).contiguous(), kc, vc, meta.block_tables, meta.start_pos, cu,
+                                work, alibi, window, scale)
+    return o.view(B, n, Hq, D)
+
+
+def _kv_append_ragged(k, v, kc, vc, meta):
+    """Host / non-bf16 path: k, v [T, Hk, D] into the paged cache at each token's (sequence, position)."""
+    BS = kc.shape[2]
+    slots = meta.pos_ids.long()
+    blk = meta.block_tables.long()[meta.seq_ids.long(), slots // BS]
+    kc[blk, :, slots % BS] = k.to(kc.dtype)
+    vc[blk, :, slots % BS] = v.to(vc.dtype)
+
+
+def _ragged_attention(q, kc, vc, meta, scale, alibi, window):
+    """q [T, Hq, D] -> [T, Hq, D] over the paged cache (new tokens already appended)."""
+    T, Hq, D = q.shape
+    nd, S = meta.n_decode, len(meta.start_host)
+    fast = q.is_cuda and q.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16
+    from ...ops.native import hip_ops
+    if fast and D == 128 and nd < S:
+        out = hip_ops().paged_prefill(q.contiguous(), kc, vc, meta.block_tables, meta.start_pos, meta.cu_q, meta.work,
+                                      alibi, window, scale)
+    else:
+        out = torch.empty_like(q)
+        for i in range(nd, S):
+            a, b = meta.cu_host[i], meta.cu_host[i + 1]
+            out[a:b] = _seq_cached_attention(q[a:b], kc, vc, meta, i, scale, alibi, window)
+    if nd:
+        if fast and D in (64, 128, 256):
+            out[:nd] = hip_ops().paged_decode(q[:nd].contiguous(), kc, vc, meta.block_tables[:nd], meta.seq_lens[:nd],
+                                              meta.max_len, scale, alibi, window)
+        else:
+            for i in range(nd):
+                out[i:i + 1] = _seq_cached_attention(q[i:i + 1], kc, vc, meta, i, scale, alibi, window)
+    return out
+
+
+def _seq_cached_attention(q, kc, vc, meta, i, scale, alibi, window):
+    """Reference path for one ragged sequence: q [n, Hq, D] at positions start..start+n-1 over its cached keys."""
+    n, Hq, D = q.shape
+    st = meta.start_host[i]
+    L = st + n
+    BS = kc.shape[2]
+    nblk = -(-L // BS)
+    ids = meta.block_tables[i, :nblk].long()
+    k = kc[ids].transpose(0, 1).reshape(kc.shape[1], nblk * BS, D)[:, :L]
+    v = vc[ids].transpose(0, 1).reshape(vc.shape[1], nblk * BS, D)[:, :L]
+    rep = Hq // k.shape[0]
+    if rep > 1:
+        k, v = k.repeat_interleave(rep, 0), v.repeat_interleave(rep, 0)
+    qpos = torch.arange(st, L, device=q.device)
+    kpos = torch.arange(L, device=q.device)
+    bad = kpos[None, :] > qpos[:, None]
+    if window:
+        bad = bad | (kpos[None, :] <= qpos[:, None] - window)
+    mask = torch.zeros(Hq if alibi is not None else 1, n, L, device=q.device, dtype=torch.float32)
+    if alibi is not None:
+        mask = mask + _alibi_bias(alibi, qpos, L, q.device)
+    mask = mask.masked_fill(bad[None], float("-inf")).to(q.dtype)
+    o = F.scaled_dot_product_attention(q.transpose(0, 1).unsqueeze(0), k.unsqueeze(0).to(q.dtype),
+                                       v.unsqueeze(0).to(q.dtype), attn_mask=mask.unsqueeze(0), scale=scale)
+    return o[0].transpose(0, 1)
+
+
 def _decode_attention(q, kc, vc, meta, scale, alibi, window):
     if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128, 256):
         from ...ops.native import hip_ops
@@ -502,6 +661,32 @@ class DSInferenceModel(nn.Module):
                 logits = hip_ops().skinny_gemm(h, self.lm_head, self.lm_head_b, None, 1, False, 0, residual,
                                                self.norm_w, self.spec.norm_eps, None)
                 return self._gather_vocab(logits)
+        x = h if residual is None else h + residual
+        if self.spec.final_norm:
+            if self.spec.norm == "rms":
+                x = DF.rms_norm(x, self.norm_w, self.spec.norm_eps)
+            else:
+                x = DF.layer_norm(x, self.norm_w, self.norm_b, self.spec.norm_eps)
+        return self._logits(x)
+
+    @torch.no_grad()
+    def forward_ragged(self, tokens, meta: RaggedMeta):
+        """tokens [T] (every sequence's new tokens, concatenated as in `meta`) -> logits [S, V] of each sequence's
+        last token. One forward for the whole ragged batch (inference v2 `put()`)."""
+        ids = tokens.view(1, -1)
+        h = self._embed(ids, meta)
+        residual = None
+        rope = (self.rope_cos, self.rope_sin)
+        for layer in self.layers:
+            h, residual = layer(h, residual, meta, self.cache, rope, self.alibi)
+        h = h[0].index_select(0, meta.last_idx)
+        residual = residual[0].index_select(0, meta.last_idx) if residual is not None else None
+        if (h.is_cuda and h.dtype == torch.bfloat16 and self.spec.final_norm and self.spec.norm == "rms"
+                and _skinny_rows_ok(h.shape[0], self.spec.hidden_size)):
+            from ...ops.native import hip_ops
+            logits = hip_ops().skinny_gemm(h, self.lm_head, self.lm_head_b, None, 1, False, 0, residual, self.norm_w,
+                                           self.spec.norm_eps, None)
+            return self._gather_vocab(logits)
         x = h if residual is None else h + residual
         if self.spec.final_norm:
             if self.spec.norm == "rms":

@@ -1,17 +1,20 @@
 """Ragged-batching inference engine (reference `inference/v2/engine_v2.py:30-240`, FastGen's put / query /
 can_schedule / flush contract).
 
-`put(uids, tokens)` runs ONE scheduling step over a ragged batch: sequences contributing a single token (decode)
-are batched into one forward over the paged KV cache (HIP paged-decode kernel, HIP skinny GEMMs); prompt or
-prompt-chunk sequences (SplitFuse-style chunks of any length, continuing from their cached prefix) run as prefill
-forwards. It returns one row of logits per sequence, in the order given. KV blocks are allocated on demand from a
-per-engine block pool sized from free HBM (RESERVE mode) or an explicit block count (ALLOCATE mode).
+`put(uids, tokens)` runs ONE scheduling step over a ragged batch as ONE forward (reference `ragged_wrapper.py:31-193`
++ `engine_v2.py:107-153`): the new tokens of every sequence — single-token decodes first, then prompts and
+SplitFuse prompt chunks of any length continuing from their cached prefix — are concatenated; the GEMMs run over all
+T tokens at once, the fused QKV epilogue appends every token's K/V to the paged cache, the paged decode kernel
+serves the decode rows and the ragged paged flash-prefill kernel (`csrc/attn/paged_prefill.hip`) the chunk rows.
+All per-step metadata goes to the device in one packed copy; nothing syncs back to the host. It returns one row of
+logits per sequence, in the order given. KV blocks are allocated on demand from a per-engine block pool sized from
+free HBM (RESERVE mode) or an explicit block count (ALLOCATE mode).
 """
 from typing import Iterable, Tuple
 
 import torch
 
-from ..model_implementations.transformer import BatchMeta, DSInferenceModel
+from ..model_implementations.transformer import DSInferenceModel, RaggedMeta
 from .config_v2 import AllocationMode, RaggedInferenceEngineConfig
 from .ragged import DSStateManager, PlaceholderSequenceDescriptor
 from .scheduling_utils import SchedulingError, SchedulingResult
@@ -54,16 +57,6 @@ class InferenceEngineV2:
         return self._model
 
     # ------------------------------------------------------------------------------------------ forward
-    def _meta(self, seqs, n_new):
-        dev = self._device
-        starts = [s.seen_tokens for s in seqs]
-        st = torch.tensor(starts, dtype=torch.int32, device=dev)
-        pos = (st[:, None] + torch.arange(n_new, dtype=torch.int32, device=dev)[None]).reshape(-1).contiguous()
-        bt = self._state_manager.block_table(seqs, dev)
-        return BatchMeta(block_tables=bt, start_pos=st, seq_lens=st + n_new, pos_ids=pos, n_new=n_new,
-                         max_len=bt.shape[1] * self._state_manager.block_size,
-                         prefill_from_zero=all(s == 0 for s in starts))
-
     @torch.no_grad()
     def put(self, batch_uids: Iterable[int], batch_tokens: Iterable[torch.Tensor], do_checks=True) -> torch.Tensor:
         uids = list(batch_uids)
@@ -78,21 +71,21 @@ class InferenceEngineV2:
             self._state_manager.allocate_blocks(seq, t.numel())
             seq.pre_forward(t.numel())
             seqs.append(seq)
-        out = [None] * len(uids)
-        decode = [i for i, (s, t) in enumerate(zip(seqs, toks)) if t.numel() == 1 and s.seen_tokens > 0]
-        if decode:
-            ds = [seqs[i] for i in decode]
-            ids = torch.stack([toks[i] for i in decode]).to(self._device).view(len(decode), 1)
-            logits = self._model(ids, self._meta(ds, 1))
-            for j, i in enumerate(decode):
-                out[i] = logits[j]
-        for i in range(len(uids)):
-            if out[i] is None:  # prompt / prompt chunk
-                ids = toks[i].to(self._device).view(1, -1)
-                out[i] = self._model(ids, self._meta([seqs[i]], ids.shape[1]))[0]
+        # decode sequences first (the paged decode kernel takes a leading slice), then prompts / chunks
+        order = sorted(range(len(uids)), key=lambda i: 0 if (toks[i].numel() == 1 and seqs[i].seen_tokens > 0) else 1)
+        n_decode = sum(1 for i in order if toks[i].numel() == 1 and seqs[i].seen_tokens > 0)
+        oseqs = [seqs[i] for i in order]
+        meta = RaggedMeta.build([s.seen_tokens for s in oseqs], [toks[i].numel() for i in order],
+                                [s.blocks for s in oseqs], n_decode, self._state_manager.block_size, self._device)
+        ids = torch.cat([toks[i] for i in order]).to(self._device, non_blocking=True)
+        logits = self._model.forward_ragged(ids, meta)
+        inv = [0] * len(order)
+        for j, i in enumerate(order):
+            inv[i] = j
+        out = logits.index_select(0, torch.tensor(inv, device=logits.device))
         for s in seqs:
             s.post_forward()
-        return torch.stack(out)
+        return out
 
     # ------------------------------------------------------------------------------------------ scheduling
     def _kv_requirements(self, seq, max_tokens, max_blocks):

@@ -231,12 +231,15 @@ __global__ void __launch_bounds__(256) qkv_rope_append_kernel(
     const bf16* __restrict__ qkv, const float* __restrict__ cosT, const float* __restrict__ sinT,
     const int* __restrict__ pos, bf16* __restrict__ q_out, bf16* __restrict__ k_out, bf16* __restrict__ v_out,
     bf16* __restrict__ kc, bf16* __restrict__ vc, const int* __restrict__ block_table,
-    const int* __restrict__ start_pos, int n_new, int Hq, int Hk, int D, int rot, int interleaved, int BS,
-    int max_blocks) {
+    const int* __restrict__ start_pos, const int* __restrict__ seq_ids, int n_new, int Hq, int Hk, int D, int rot,
+    int interleaved, int BS, int max_blocks) {
   // grid = (tokens, head groups): 256 threads cover 256 / (D/2) heads of one token, one thread per element pair
   const int H3 = Hq + 2 * Hk, half = D / 2, rh = rot / 2;
   const int tph = half < (int)blockDim.x ? half : (int)blockDim.x;
-  const int t = blockIdx.x, h = blockIdx.y * (blockDim.x / tph) + threadIdx.x / tph, b = t / n_new, j = t % n_new;
+  // uniform batch: token t is row t % n_new of sequence t / n_new; ragged batch (seq_ids): sequence seq_ids[t],
+  // cache slot = its position
+  const int t = blockIdx.x, h = blockIdx.y * (blockDim.x / tph) + threadIdx.x / tph;
+  const int b = seq_ids ? seq_ids[t] : t / n_new, j = seq_ids ? 0 : t % n_new;
   if (h >= H3) return;
   const bf16* src = qkv + ((int64_t)t * H3 + h) * D;
   bf16* dst;
@@ -246,7 +249,7 @@ __global__ void __launch_bounds__(256) qkv_rope_append_kernel(
   } else {
     const bool isk = h < Hq + Hk;
     const int kh = isk ? h - Hq : h - Hq - Hk;
-    const int slot = start_pos[b] + j;
+    const int slot = seq_ids ? pos[t] : start_pos[b] + j;
     const int blk = block_table[(int64_t)b * max_blocks + slot / BS], off = slot % BS;
     dst = (isk ? kc : vc) + (((int64_t)blk * Hk + kh) * BS + off) * D;
     if (isk ? k_out : v_out) extra = (isk ? k_out : v_out) + ((int64_t)t * Hk + kh) * D;
@@ -328,13 +331,13 @@ extern "C" int ds_kv_append(const void* k, const void* v, void* kc, void* vc, co
 
 extern "C" int ds_qkv_rope_append(const void* qkv, const float* cosT, const float* sinT, const int* pos, void* q_out,
                                   void* k_out, void* v_out, void* kc, void* vc, const int* block_table,
-                                  const int* start_pos, int T, int n_new, int Hq, int Hk, int D, int rot,
-                                  int interleaved, int BS, int max_blocks, hipStream_t s) {
+                                  const int* start_pos, const int* seq_ids, int T, int n_new, int Hq, int Hk, int D,
+                                  int rot, int interleaved, int BS, int max_blocks, hipStream_t s) {
   if (D % 2 || rot % 2 || rot > D || (D - rot) % 2 || T <= 0) return T == 0 ? 0 : (int)hipErrorInvalidValue;
   const int tph = D / 2 < 256 ? D / 2 : 256, hpb = 256 / tph;
   hipLaunchKernelGGL(qkv_rope_append_kernel, dim3(T, (Hq + 2 * Hk + hpb - 1) / hpb), dim3(256), 0, s, (const bf16*)qkv, cosT, sinT, pos,
-                     (bf16*)q_out, (bf16*)k_out, (bf16*)v_out, (bf16*)kc, (bf16*)vc, block_table, start_pos, n_new,
-                     Hq, Hk, D, rot, interleaved, BS, max_blocks);
+                     (bf16*)q_out, (bf16*)k_out, (bf16*)v_out, (bf16*)kc, (bf16*)vc, block_table, start_pos, seq_ids,
+                     n_new, Hq, Hk, D, rot, interleaved, BS, max_blocks);
   DS_CHECK_LAUNCH();
   return 0;
 }

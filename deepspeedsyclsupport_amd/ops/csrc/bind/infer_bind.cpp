@@ -18,7 +18,9 @@ int ds_skinny_mfma(const void*, const void*, const void*, const void*, const voi
                    int, int, int, int, float, hipStream_t);
 int ds_rms_fwd(const void*, const void*, const void*, void*, void*, float*, int64_t, int, float, int, hipStream_t);
 int ds_qkv_rope_append(const void*, const float*, const float*, const int*, void*, void*, void*, void*, void*,
-                       const int*, const int*, int, int, int, int, int, int, int, int, int, hipStream_t);
+                       const int*, const int*, const int*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ds_paged_prefill(const void*, const void*, const void*, void*, const int*, const int*, const int*, const int*, int,
+                     const float*, int, int, int, int, int, float, hipStream_t);
 int ds_paged_decode(const void*, const void*, const void*, const int*, const int*, const float*, float*, float*, void*,
                     int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int ds_kv_append(const void*, const void*, void*, void*, const int*, const int*, int, int, int, int, int, int,
@@ -200,13 +202,18 @@ Tensor skinny_gemm(Tensor x, Tensor w, OptT bias, OptT add, int64_t in_mode, boo
 // qkv [T, (Hq+2Hk)*D] -> q [T, Hq, D] roped; k (roped) / v scattered into the paged cache; optional k/v copies.
 std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, Tensor kc, Tensor vc,
                                     Tensor block_table, Tensor start_pos, int64_t n_new, int64_t Hq, int64_t Hk,
-                                    int64_t rot, bool interleaved, bool want_kv) {
+                                    int64_t rot, bool interleaved, bool want_kv, OptT seq_ids) {
   need(qkv, "qkv"); need(pos, "pos"); need(kc, "kc"); need(vc, "vc"); need(block_table, "block_table");
   need(start_pos, "start_pos");
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && kc.scalar_type() == at::kBFloat16, "bf16 qkv / cache");
   const int D = (int)kc.size(3);
   const int64_t T = qkv.numel() / ((Hq + 2 * Hk) * D);
-  TORCH_CHECK(T * (Hq + 2 * Hk) * D == qkv.numel() && T % n_new == 0, "qkv shape");
+  const bool ragged = seq_ids.has_value() && seq_ids->defined();
+  TORCH_CHECK(T * (Hq + 2 * Hk) * D == qkv.numel() && (ragged || T % n_new == 0), "qkv shape");
+  if (ragged) {
+    need(*seq_ids, "seq_ids");
+    TORCH_CHECK(seq_ids->scalar_type() == at::kInt && seq_ids->numel() == T && pos.numel() == T, "seq_ids / pos [T]");
+  }
   TORCH_CHECK(kc.size(1) == Hk, "cache kv heads");
   TORCH_CHECK(rot == 0 || (cos.has_value() && sin.has_value()), "rope tables required");
   auto q = torch::empty({T, Hq, D}, qkv.options());
@@ -218,7 +225,8 @@ std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, 
   check(ds_qkv_rope_append(qkv.data_ptr(), rot ? cos->data_ptr<float>() : nullptr,
                            rot ? sin->data_ptr<float>() : nullptr, pos.data_ptr<int>(), q.data_ptr(),
                            want_kv ? k.data_ptr() : nullptr, want_kv ? v.data_ptr() : nullptr, kc.data_ptr(),
-                           vc.data_ptr(), block_table.data_ptr<int>(), start_pos.data_ptr<int>(), (int)T, (int)n_new,
+                           vc.data_ptr(), block_table.data_ptr<int>(), start_pos.data_ptr<int>(),
+                           ragged ? seq_ids->data_ptr<int>() : nullptr, (int)T, (int)n_new,
                            (int)Hq, (int)Hk, D, (int)rot, interleaved ? 1 : 0, (int)kc.size(2),
                            (int)block_table.size(1), stream()),
         "qkv_rope_append");
@@ -309,7 +317,39 @@ Tensor dequant_sh(Tensor qsh, Tensor ssh, int64_t N, int64_t gs) {
   return w;
 }
 
+// Ragged paged flash prefill (attn/paged_prefill.hip): q [T, Hq, 128] bf16, caches [blocks, Hk, BS, 128],
+// block_table [nseq, max_blocks], start [nseq], cu_q [nseq + 1], work [nwork, 2] int32 built by the caller from the
+// same lengths (every (sequence, 128-row block) with block * 128 < that sequence's new tokens).
+Tensor paged_prefill(Tensor q, Tensor kc, Tensor vc, Tensor block_table, Tensor start, Tensor cu_q, Tensor work,
+                     OptT alibi, int64_t window, double scale) {
+  need(q, "q"); need(kc, "k_cache"); need(vc, "v_cache"); need(block_table, "block_table"); need(start, "start");
+  need(cu_q, "cu_q"); need(work, "work");
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 && kc.scalar_type() == at::kBFloat16 && q.dim() == 3 && q.size(2) == 128,
+              "paged_prefill: bf16 q [T, Hq, 128]");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(3) == 128 && vc.sizes() == kc.sizes(), "paged_prefill: caches [NB, Hk, BS, 128]");
+  TORCH_CHECK(block_table.scalar_type() == at::kInt && start.scalar_type() == at::kInt && cu_q.scalar_type() == at::kInt &&
+              work.scalar_type() == at::kInt, "paged_prefill: int32 tables");
+  const int64_t nseq = start.numel();
+  TORCH_CHECK(block_table.dim() == 2 && block_table.size(0) == nseq && cu_q.numel() == nseq + 1, "paged_prefill: tables");
+  TORCH_CHECK(work.dim() == 2 && work.size(1) == 2, "paged_prefill: work [nwork, 2]");
+  const int Hq = (int)q.size(1), Hk = (int)kc.size(1);
+  TORCH_CHECK(Hq % Hk == 0, "paged_prefill: GQA ratio");
+  const float* al = nullptr;
+  if (alibi.has_value() && alibi->defined()) {
+    need(*alibi, "alibi");
+    TORCH_CHECK(alibi->scalar_type() == at::kFloat && alibi->numel() == Hq, "paged_prefill: alibi [Hq] fp32");
+    al = alibi->data_ptr<float>();
+  }
+  auto o = torch::empty_like(q);
+  check(ds_paged_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), o.data_ptr(), block_table.data_ptr<int>(),
+                         start.data_ptr<int>(), cu_q.data_ptr<int>(), work.data_ptr<int>(), (int)work.size(0), al, Hq,
+                         Hk, (int)kc.size(2), (int)block_table.size(1), (int)window, (float)scale, stream()),
+        "paged_prefill");
+  return o;
+}
+
 void register_inference_ops(pybind11::module& m) {
+  m.def("paged_prefill", &paged_prefill);
   m.def("dequant_sh", &dequant_sh);
   m.def("skinny_i8_ok", &skinny_i8_ok);
   m.def("skinny_i8_sh_ok", &skinny_i8_sh_ok);
@@ -322,7 +362,9 @@ void register_inference_ops(pybind11::module& m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_force_valu", &skinny_force_valu);
   m.def("skinny_set_path", &skinny_set_path);
-  m.def("qkv_rope_append", &qkv_rope_append);
+  m.def("qkv_rope_append", &qkv_rope_append, py::arg("qkv"), py::arg("cos"), py::arg("sin"), py::arg("pos"),
+        py::arg("kc"), py::arg("vc"), py::arg("block_table"), py::arg("start_pos"), py::arg("n_new"), py::arg("Hq"),
+        py::arg("Hk"), py::arg("rot"), py::arg("interleaved"), py::arg("want_kv"), py::arg("seq_ids") = py::none());
   m.def("paged_decode", &paged_decode);
   m.def("kv_append", &kv_append);
   m.def("quantize", &quantize);

@@ -42,6 +42,7 @@ EXTENSIONS = {
             "attn/decode_attn.hip",
             "attn/flash_fwd.hip",
             "attn/flash_bwd.hip",
+            "attn/paged_prefill.hip",
             "quant/quant_kernels.hip",
             "gemv/skinny_gemm.hip",
             "gemv/skinny_mfma.hip",

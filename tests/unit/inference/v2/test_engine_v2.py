@@ -96,11 +96,13 @@ def test_scheduling_limits():
 
 
 @pytest.mark.gpu
-def test_ragged_bf16_gpu():
-    m = _model(H=256)
+@pytest.mark.parametrize("H", [256, 512])  # head dim 64 (reference attention path) and 128 (paged flash prefill)
+def test_ragged_bf16_gpu(H):
+    m = _model(H=H)
     eng = _engine(m, dtype=torch.bfloat16, device=torch.device("cuda"), blocks=128, bs=16)
     g = torch.Generator().manual_seed(2)
-    prompts = {1: torch.randint(0, 128, (11, ), generator=g), 2: torch.randint(0, 128, (4, ), generator=g)}
+    prompts = {1: torch.randint(0, 128, (11, ), generator=g), 2: torch.randint(0, 128, (4, ), generator=g),
+               3: torch.randint(0, 128, (100, ), generator=g)}
     outs = _drive(eng, prompts, 5, chunk=6)
     # bf16 vs fp32 HF may flip near-ties: require the first token and most of the rest to agree
     for u, p in prompts.items():
