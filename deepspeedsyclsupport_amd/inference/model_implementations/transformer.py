@@ -213,6 +213,9 @@ class DSInferenceLayer(nn.Module):
         self.fc1_b = nn.Parameter(torch.zeros(G * I, **kw), requires_grad=False) if spec.mlp_bias and not E else None
         self.fc2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.mlp_bias and not E else None
         self.quant = {}
+        # split (aliased) projections: name -> list of weights / biases applied side by side (hybrid engine shares
+        # the training module's separate q/k/v and gate/up tensors instead of fusing copies)
+        self.split_w, self.split_b = {}, {}
 
     # ------------------------------------------------------------------------------------------ helpers
     def quantize_weights(self, bits=8, group_size=64):
@@ -226,6 +229,9 @@ class DSInferenceLayer(nn.Module):
         fused-dequant MFMA stream over the pre-shuffled weight (`csrc/gemv/skinny_int8.hip`, never materialises a
         bf16 weight); larger batches dequantise into a bf16 temporary for a library GEMM (reference
         `ds_vector_matmul_int8`)."""
+        if name in self.split_w:
+            bs = self.split_b.get(name) or [None] * len(self.split_w[name])
+            return torch.cat([F.linear(x, w, b) for w, b in zip(self.split_w[name], bs)], -1)
         qw = self.quant.get(name)
         if qw is not None and qw.i8 is not None:
             return qw.i8.linear(x, bias)
@@ -356,7 +362,7 @@ class DSInferenceLayer(nn.Module):
     # ------------------------------------------------------------------------------------------ decode fast path
     def _skinny_ok(self, h):
         spec = self.spec
-        return (h.is_cuda and h.dtype == torch.bfloat16 and not self.quant and spec.norm == "rms"
+        return (h.is_cuda and h.dtype == torch.bfloat16 and not self.quant and not self.split_w and spec.norm == "rms"
                 and not spec.parallel_residual and not spec.num_experts and _skinny_rows_ok(h.numel() // h.shape[-1], spec.hidden_size,
                                                                     spec.intermediate_size // self.tp,
                                                                     self.hq * spec.head_dim))

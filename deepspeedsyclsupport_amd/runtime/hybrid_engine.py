@@ -2,13 +2,21 @@
 and generates (kernel-injected inference) with the SAME weights.
 
 generate():
-  1. (ZeRO-3) gather the partitioned parameters once for the whole rollout;
-  2. fuse LoRA adapters into the base weights (modules exposing fuse_lora_weight / unfuse_lora_weight, the
+  1. fuse LoRA adapters into the base weights (modules exposing fuse_lora_weight / unfuse_lora_weight, the
      DeepSpeed-Chat convention);
-  3. refresh a persistent `DSInferenceModel` built from the training module (paged KV cache, HIP decode kernels,
-     optional HIP-graph decode) — refresh is a device-to-device weight copy, no re-conversion;
-  4. generate, then unfuse LoRA and release the gathered parameters (and, with release_inference_cache, the cache).
-Models without an injection policy fall back to the module's own `generate` under the gathered parameters.
+  2. make the persistent `DSInferenceModel` (paged KV cache, HIP decode kernels, optional HIP-graph decode) hold the
+     current weights:
+       * ZeRO-0/1/2 with inference_tp_size 1: it SHARES the training tensors — every inference weight is an alias of
+         the module's parameter (q/k/v and gate/up stay separate tensors applied side by side), so the optimizer's
+         in-place updates and LoRA fusing are visible without any copy and no second weight set exists;
+       * ZeRO-3 and/or inference_tp_size > 1 (reference `hybrid_engine.py:115,183-230,316-337`): a TP-sharded
+         inference model (1/tp of the weights per rank) refilled ONE LAYER AT A TIME — gather that layer's partitions,
+         copy this rank's shard, release — and only when the weights changed (optimizer step / LoRA) since the last
+         refresh;
+  3. with inference_tp_size > 1 the ranks of a TP group pool their prompts, generate together on the sharded model
+     (RCCL all-reduce per block) and each keeps its own rows;
+  4. unfuse LoRA (and, with release_inference_cache, drop the KV cache).
+Models without an injection policy fall back to the module's own `generate` under fully gathered parameters.
 """
 import time
 
@@ -48,11 +56,144 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
             m.unfuse_lora_weight()
         self.is_lora_fused = False
 
-    def _gathered(self):
+    def _gathered(self, params=None):
         if self.zero_optimization_partition_weights():
             from .zero.partition_parameters import GatheredParameters
-            return GatheredParameters(list(self.module.parameters()))
+            return GatheredParameters(list(self.module.parameters()) if params is None else list(params))
         return _Null()
+
+    def _tp(self):
+        """(group, size, rank) of this rank's inference TP group: consecutive ranks, created collectively once."""
+        if not hasattr(self, "_tp_info"):
+            tp = max(int(self.hcfg.inference_tp_size), 1)
+            world, rank = dist.get_world_size(), dist.get_rank()
+            if tp == 1 or world == 1:
+                self._tp_info = (None, 1, 0)
+            else:
+                if world % tp:
+                    raise ValueError(f"inference_tp_size {tp} must divide the world size {world}")
+                mine = None
+                for g in range(world // tp):
+                    grp = dist.new_group(list(range(g * tp, (g + 1) * tp)))
+                    if g == rank // tp:
+                        mine = grp
+                self._tp_info = (mine, tp, rank % tp)
+        return self._tp_info
+
+    def _layer_container(self, num_layers):
+        """The ModuleList holding the decoder layers (per-layer gathers under ZeRO-3)."""
+        for _, m in self.module.named_modules():
+            if isinstance(m, torch.nn.ModuleList) and len(m) == num_layers:
+                return m
+        return None
+
+    def _weights_version(self):
+        return (getattr(self, "global_steps", 0), self.is_lora_fused, id(self))
+
+    def _share_into(self, ds, spec, top, layers):
+        """Alias the inference model's weights to the training tensors (ZeRO-0/1/2, TP 1): no copy. The model was
+        built on the meta device, so each parameter is REPLACED by one wrapping the training tensor's storage."""
+        dev = self.device
+
+        def put(mod, name, t):
+            if getattr(mod, name, None) is None or t is None:
+                return
+            mod._parameters[name] = torch.nn.Parameter(t, requires_grad=False)
+
+        def alias(mod, name, src):
+            p = getattr(mod, name, None)
+            if p is None or src is None:
+                return
+            src = src.detach()
+            if src.dtype != p.dtype or src.shape != p.shape:  # (rare) dtype / shape mismatch: own copy
+                src = src.to(dtype=p.dtype, device=dev).reshape(p.shape).clone()
+            put(mod, name, src)
+
+        for layer, lw in zip(ds.layers, layers):
+            layer.split_w["qkv_w"] = [lw["q_w"].detach(), lw["k_w"].detach(), lw["v_w"].detach()]
+            if lw.get("q_b") is not None:
+                layer.split_b["qkv_w"] = [lw["q_b"], lw["k_b"], lw["v_b"]]
+            fused_mlp = "gate_w" in lw
+            if fused_mlp:
+                layer.split_w["fc1_w"] = [lw["gate_w"].detach(), lw["up_w"].detach()]
+                if lw.get("gate_b") is not None:
+                    layer.split_b["fc1_w"] = [lw["gate_b"], lw["up_b"]]
+            else:
+                alias(layer, "fc1_w", lw["fc1_w"])
+                alias(layer, "fc1_b", lw.get("fc1_b"))
+            for name in ("qkv_w", "qkv_b") + (("fc1_w", "fc1_b") if fused_mlp else ()):
+                p = getattr(layer, name, None)
+                if p is not None:
+                    put(layer, name, torch.empty(0, dtype=p.dtype, device=dev))
+            alias(layer, "o_w", lw["o_w"])
+            alias(layer, "o_b", lw.get("o_b"))
+            alias(layer, "fc2_w", lw["fc2_w"])
+            alias(layer, "fc2_b", lw.get("fc2_b"))
+            for n in ("ln1_w", "ln1_b", "ln2_w", "ln2_b"):
+                alias(layer, n, lw.get(n))
+            if spec.shared_parallel_norm:
+                alias(layer, "ln2_w", lw["ln1_w"])
+                alias(layer, "ln2_b", lw.get("ln1_b"))
+        alias(ds, "embed", top["embed"])
+        if spec.embed_norm:
+            alias(ds, "embed_ln_w", top["embed_ln_w"])
+            alias(ds, "embed_ln_b", top["embed_ln_b"])
+        alias(ds, "norm_w", top["norm_w"])
+        alias(ds, "norm_b", top.get("norm_b"))
+        if ds.lm_head.shape[0] == top["lm_head"].shape[0]:
+            alias(ds, "lm_head", top["lm_head"])
+            alias(ds, "lm_head_b", top.get("lm_head_b"))
+        else:  # vocab padding: keep an own padded copy
+            lm = torch.zeros(ds.lm_head.shape, dtype=ds.dtype, device=dev)
+            lm[:top["lm_head"].shape[0]].copy_(top["lm_head"].detach())
+            put(ds, "lm_head", lm)
+        if ds.pos_embed is not None:
+            pe = top["pos_embed"].detach()
+            t = torch.zeros(ds.pos_embed.shape, dtype=ds.dtype, device=dev)
+            n = min(pe.shape[0], t.shape[0])
+            t[:n].copy_(pe[:n])
+            put(ds, "pos_embed", t)
+        self._materialize(ds)
+
+    def _materialize(self, ds):
+        """Give every parameter still on the meta device real (zero) storage and rebuild the position tables."""
+        from ..inference.model_implementations.transformer import alibi_slopes
+        from ..ops import reference
+        for mod in ds.modules():
+            for name, p in list(mod._parameters.items()):
+                if p is not None and p.device.type == "meta":
+                    mod._parameters[name] = torch.nn.Parameter(
+                        torch.zeros(p.shape, dtype=p.dtype, device=self.device), requires_grad=False)
+        spec = ds.spec
+        if ds.rope_cos is not None and ds.rope_cos.device.type == "meta":
+            cos, sin = reference.rope_tables(max(spec.max_positions, 2048) * 2, spec.rotary_dim, spec.rope_theta,
+                                             device=self.device)
+            ds.rope_cos, ds.rope_sin = cos, sin
+        if ds.alibi is not None and ds.alibi.device.type == "meta":
+            hq = spec.num_heads // ds.tp_size
+            ds.alibi = alibi_slopes(spec.num_heads)[ds.tp_rank * hq:(ds.tp_rank + 1) * hq].contiguous().to(self.device)
+        ds.device = self.device
+
+    def _copy_into(self, ds, spec):
+        """TP-sharded copy, one decoder layer gathered at a time (ZeRO-3 partitions are never gathered at once)."""
+        from ..inference.model_implementations import convert
+        container = self._layer_container(spec.num_layers)
+        r, tp = ds.tp_rank, ds.tp_size
+        for i, layer in enumerate(ds.layers):
+            params = container[i].parameters() if container is not None else self.module.parameters()
+            with self._gathered(params):
+                _, _, layers = convert.extract(self.module)
+                with torch.no_grad():
+                    for name, t in convert.shard_layer(spec, layers[i], r, tp).items():
+                        p = getattr(layer, name)
+                        if p is not None and t is not None:
+                            p.data.copy_(t.detach().to(p.dtype))
+        per_layer = set(id(p) for p in container.parameters()) if container is not None else set()
+        rest = [p for p in self.module.parameters() if id(p) not in per_layer]
+        with self._gathered(rest):
+            _, top, _ = convert.extract(self.module)
+            with torch.no_grad():
+                convert.load_into(ds, top, [])
 
     def _refresh_inference_model(self):
         from ..inference.config import DeepSpeedInferenceConfig
@@ -60,17 +201,39 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
         from ..inference.model_implementations import convert
         if not convert.supported(self.module):
             return None
-        spec, top, layers = convert.extract(self.module)
+        group, tp, r = self._tp()
+        zero3 = self.zero_optimization_partition_weights()
+        share = not zero3 and tp == 1
         dtype = self._dtype() if self._dtype() in (torch.bfloat16, torch.float16) else torch.float32
         if self._ds_model is None:
             from ..inference.model_implementations.transformer import DSInferenceModel
+            spec, top, layers = convert.extract(self.module)
             spec.max_positions = max(spec.max_positions, self.hcfg.max_out_tokens)
-            self._ds_model = DSInferenceModel(spec, None, 1, 0, dtype, self.device)
+            # shared weights: build on the meta device so no second weight set is ever allocated
+            self._ds_model = DSInferenceModel(spec, group, tp, r, dtype,
+                                              torch.device("meta") if share else self.device)
+            self._loaded_version = None
+            if share:
+                self._share_into(self._ds_model, spec, top, layers)
+                self._loaded_version = "shared"
             cfg = DeepSpeedInferenceConfig(dtype=dtype, max_tokens=self.hcfg.max_out_tokens)
-            self._inference = InferenceEngine.from_ds_model(self._ds_model, cfg)
-        with torch.no_grad():
-            convert.load_into(self._ds_model, top, layers)
+            self._inference = InferenceEngine.from_ds_model(self._ds_model, cfg, tp_group=group, tp_size=tp,
+                                                            tp_rank=r)
+        if self._loaded_version != "shared" and self._loaded_version != self._weights_version():
+            self._copy_into(self._ds_model, self._ds_model.spec)
+            self._loaded_version = self._weights_version()
         return self._inference
+
+    def _tp_generate(self, inf, input_ids, **kwargs):
+        """inference_tp_size > 1: pool the TP group's prompts, generate once on the sharded model, keep own rows."""
+        group, tp, r = self._tp()
+        if tp == 1:
+            return inf.generate(input_ids, **kwargs)
+        parts = [torch.empty_like(input_ids) for _ in range(tp)]
+        dist.all_gather(parts, input_ids.contiguous(), group=group)
+        out = inf.generate(torch.cat(parts, 0), **kwargs)
+        B = input_ids.shape[0]
+        return out[r * B:(r + 1) * B]
 
     # ------------------------------------------------------------------------------------------ API
     @torch.no_grad()
@@ -80,17 +243,20 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
         was_training = self.module.training
         self.module.eval()
         try:
-            with self._gathered():
-                if self._lora_modules():
+            if self._lora_modules():
+                with self._gathered():
                     self.fuse_lora_weight()
-                try:
-                    inf = self._refresh_inference_model()
-                    if inf is not None:
-                        out = inf.generate(*inputs, **kwargs)
-                    else:
+            try:
+                inf = self._refresh_inference_model()
+                if inf is not None:
+                    ids = inputs[0] if inputs else kwargs.pop("input_ids")
+                    out = self._tp_generate(inf, ids.to(self.device), **kwargs)
+                else:
+                    with self._gathered():
                         out = self.module.generate(*inputs, **kwargs)
-                finally:
-                    if self.is_lora_fused:
+            finally:
+                if self.is_lora_fused:
+                    with self._gathered():
                         self.unfuse_lora_weight()
         finally:
             self._in_generate = False

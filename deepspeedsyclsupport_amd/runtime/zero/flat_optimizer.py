@@ -757,10 +757,11 @@ class FlatZeroOptimizer:
                         for i, lp in back:
                             lp.copy_(lps[i], non_blocking=lp.is_pinned())
                     else:
-                        from ...ops import reference
+                        # host flats (CPU accelerator / gloo): the native AVX-512 Adam (csrc/cpu/cpu_optim.cpp)
+                        cpu = native.cpu_ops()
                         for p_, m_, v_, g_, lp_ in zip(ps, ms, vs, gs, lps):
-                            reference.adam_update(p_, m_, v_, g_, group["lr"], b1, b2, group["eps"],
-                                                  group["weight_decay"], step, bc, adamw, grad_scale * s, lp_)
+                            cpu.cpu_adam_update(p_, m_, v_, g_.contiguous(), lp_, step, group["lr"], b1, b2,
+                                                group["eps"], group["weight_decay"], bc, adamw, grad_scale * s)
         else:
             # generic torch optimizer over the fp32 flats: materialise scaled fp32 grads, step, copy to shards
             for og in range(self.num_og):

@@ -44,7 +44,7 @@ class LoRALinear(torch.nn.Module):
         return y
 
 
-def _run(stage, lora, out):
+def _run(stage, lora, tp, out):
     import deepspeedsyclsupport_amd as ds
     from deepspeedsyclsupport_amd import comm as dist
     from deepspeedsyclsupport_amd.runtime.zero.partition_parameters import GatheredParameters
@@ -53,7 +53,8 @@ def _run(stage, lora, out):
         for layer in model.model.layers:
             layer.self_attn.q_proj = LoRALinear(layer.self_attn.q_proj)
     cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}},
-           "zero_optimization": {"stage": stage}, "hybrid_engine": {"enabled": True, "max_out_tokens": 64}}
+           "zero_optimization": {"stage": stage},
+           "hybrid_engine": {"enabled": True, "max_out_tokens": 64, "inference_tp_size": tp}}
     if lora:
         cfg["zero_optimization"]["stage"] = 0
     eng, _, _, _ = ds.initialize(model=model, config=cfg)
@@ -61,6 +62,14 @@ def _run(stage, lora, out):
     results = []
     for it in range(2):
         got = eng.generate(ids, max_new_tokens=5)
+        if it == 0 and stage < 3 and tp == 1:  # shared weights: the inference model aliases the training tensors
+            ds_layer = eng._ds_model.layers[0]
+            hf = eng.module.model.layers[0]
+            assert ds_layer.o_w.data_ptr() == hf.self_attn.o_proj.weight.data_ptr()
+            assert ds_layer.split_w["qkv_w"][0].data_ptr() == hf.self_attn.q_proj.weight.data_ptr()
+            assert ds_layer.qkv_w.numel() == 0
+        if tp > 1:
+            assert eng._ds_model.tp_size == tp and eng._ds_model.layers[0].hq == 4 // tp
         # oracle: plain HF generate on a copy holding the gathered training weights (LoRA folded in)
         with GatheredParameters(list(eng.module.parameters())):
             ref_model = copy.deepcopy(eng.module)
@@ -82,10 +91,10 @@ def _run(stage, lora, out):
         torch.save(results, out)
 
 
-@pytest.mark.parametrize("stage,lora", [(3, False), (2, False), (0, True)])
-def test_hybrid_generate_tracks_training(stage, lora, tmp_path):
+@pytest.mark.parametrize("stage,lora,tp", [(3, False, 1), (2, False, 1), (0, True, 1), (3, False, 2), (2, False, 2)])
+def test_hybrid_generate_tracks_training(stage, lora, tp, tmp_path):
     out = str(tmp_path / "h.pt")
-    run_distributed(_run, 2, stage, lora, out)
+    run_distributed(_run, 2, stage, lora, tp, out)
     results = torch.load(out, weights_only=True)
     for got, ref in results:
         assert torch.equal(got, ref)
