@@ -66,6 +66,7 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
                                  training_data=training_data, lr_scheduler=lr_scheduler, mpu=mpu,
                                  dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
                                  config_class=cfg)
+    zero.partition_parameters.restore_init_context()
     return engine, engine.optimizer, engine.training_dataloader, engine.lr_scheduler
 
 

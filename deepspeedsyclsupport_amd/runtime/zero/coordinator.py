@@ -54,6 +54,48 @@ class ParamCoordinator:
             self._hooks.append(m.register_forward_pre_hook(self._pre_fwd))
             self._hooks.append(m.register_forward_hook(self._post_fwd))
             self._hooks.append(m.register_full_backward_pre_hook(self._pre_bwd))
+        for m in opt.module.modules():
+            if m.__dict__.get("_ds_external_params"):
+                self.install_external(m)
+
+    # ----------------------------------------------------------------------------------- external parameters
+    def install_external(self, m):
+        """Fetch hooks for the parameters `m` uses but does not own (`zero.register_external_parameter`). A group
+        already gathered by its owner (nested use) is borrowed, not released, by `m`."""
+        if m.__dict__.get("_ds_ext_hooked"):
+            return
+        m.__dict__["_ds_ext_hooked"] = True
+
+        def groups_of(mod):
+            seen, out = set(), []
+            for p in mod.__dict__.get("_ds_external_params", []):
+                g = getattr(p, "ds_group", None)
+                if g is not None and not g.persistent and id(g) not in seen:
+                    seen.add(id(g))
+                    out.append(g)
+            return out
+
+        def pre(mod, inputs):
+            mod.__dict__["_ds_ext_borrowed"] = {g.idx: g.status != ZeroParamStatus.NOT_AVAILABLE
+                                                for g in groups_of(mod)}
+            for g in groups_of(mod):
+                self.fetch(g)
+
+        def post(mod, inputs, outputs):
+            if self.in_backward or torch._C._current_graph_task_id() != -1:
+                return
+            borrowed = mod.__dict__.get("_ds_ext_borrowed", {})
+            for g in groups_of(mod):
+                if not borrowed.get(g.idx, False):
+                    self.release(g)
+
+        def pre_bwd(mod, grad_output):
+            for g in groups_of(mod):
+                self.fetch(g)
+
+        self._hooks.append(m.register_forward_pre_hook(pre))
+        self._hooks.append(m.register_forward_hook(post))
+        self._hooks.append(m.register_full_backward_pre_hook(pre_bwd))
 
     # ----------------------------------------------------------------------------------- hooks
     def _pre_fwd(self, m, inputs):

@@ -159,8 +159,11 @@ class FlatZeroOptimizer:
             from ..swap_tensor import OptimizerStateSwapper
             path = self.zc.offload_optimizer.nvme_path or "/tmp/ds_nvme_swap"
             folder = os.path.join(path, f"zero_stage_{self.stage}", "optimizer", f"rank{dist.get_rank()}")
-            self.nvme_swapper = OptimizerStateSwapper(ds_config.aio_config, folder,
-                                                      pin=self.device.type == "cuda")
+            # ZeRO-Infinity: the fp32 master AND the moments of the host partition live on NVMe, streamed in
+            # sub_group_size chunks (reference partitioned_optimizer_swapper: fp32 params + optimizer states)
+            chunk = int(min(getattr(self.zc, "sub_group_size", 64 * 2**20) or 64 * 2**20, 64 * 2**20))
+            self.nvme_swapper = OptimizerStateSwapper(ds_config.aio_config, folder, chunk_numel=max(chunk, 1),
+                                                      pin=self.device.type == "cuda", with_master=True)
         # ZeRO-Infinity parameter offload: non-persistent ZeRO-3 shards live in pinned host memory (cpu) or in
         # per-group files on NVMe mapped into the address space (nvme); every fetch streams them H2D on the
         # all-gather stream ahead of use (trace-driven prefetch), so HBM only holds the live working set.
@@ -306,10 +309,12 @@ class FlatZeroOptimizer:
                 del full, seg
                 g.full = None
                 self._release_params(g)
+            from .partition_parameters import _attach_api
             for i, p in enumerate(g.params):
                 p.ds_numel = g.numels[i]
                 p.ds_persist = g.persistent
                 p.ds_group = g
+                _attach_api(p)
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
 
@@ -376,13 +381,33 @@ class FlatZeroOptimizer:
                 dev_len[og] += n
             g.runs.append((s - g.seg_lo, e - g.seg_lo, og, moff, on_host))
         pin = self.device.type == "cuda" and self.offload and getattr(self, "offload_pin", True)
+        host_runs = [[] for _ in range(self.num_og)]
+        for g in self.groups:
+            for (s, e, og, moff, on_host) in g.runs:
+                if on_host:
+                    host_runs[og].append((moff, e - s, g, s))
         for og in range(self.num_og):
             self.master.append(torch.zeros(dev_len[og], dtype=torch.float32, device=self.device))
             self.grad_acc.append(None)  # fp32 accumulator, allocated only when a path needs it
-            self.master_host.append(_host_zeros(host_len[og], torch.float32, pin) if host_len[og] else None)
+            if host_len[og] and self.nvme_swapper is not None:
+                from ..swap_tensor.optimizer_swapper import NvmeFlat
+
+                def init(lo, hi, buf, runs=host_runs[og]):  # fill one chunk of the master from the shards
+                    buf.zero_()
+                    for moff, n, g, s in runs:
+                        a, b = max(lo, moff), min(hi, moff + n)
+                        if a < b:
+                            buf[a - lo:b - lo].copy_(g.shard[s + a - moff:s + b - moff])
+
+                self.nvme_swapper.register(og, host_len[og], master_init=init)
+                self.master_host.append(NvmeFlat(self.nvme_swapper, og, host_len[og]))
+            else:
+                self.master_host.append(_host_zeros(host_len[og], torch.float32, pin) if host_len[og] else None)
             self.grad_acc_host.append(_host_zeros(host_len[og], torch.float32, pin) if host_len[og] else None)
         for g in self.groups:
             for (s, e, og, moff, on_host) in g.runs:
+                if on_host and self.nvme_swapper is not None:
+                    continue  # written into the NVMe master above
                 dst = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
                 dst.copy_(g.shard[s:e])
         # hand the fp32 buffers to the wrapped optimizer (its param_groups / lr schedule stay authoritative)
@@ -801,12 +826,12 @@ class FlatZeroOptimizer:
             bc = group.get("bias_correction", True)
             gr = self.grad_acc_host[og]
             if self.nvme_swapper is not None:
-                # ZeRO-Infinity: moments stream from NVMe chunk by chunk (read-ahead / write-behind)
+                # ZeRO-Infinity: master + moments stream from NVMe chunk by chunk (read-ahead / write-behind)
                 if og not in self.nvme_swapper.sizes:
                     self.nvme_swapper.register(og, hp.numel())
 
-                def upd(lo, hi, m, v, step, hp=hp, lp=lp, gr=gr, group=group, b1=b1, b2=b2):
-                    cpu_ops().cpu_adam_update(hp[lo:hi], m, v, gr[lo:hi], lp[lo:hi], step, group["lr"], b1, b2,
+                def upd(lo, hi, m, v, step, master, lp=lp, gr=gr, group=group, b1=b1, b2=b2):
+                    cpu_ops().cpu_adam_update(master, m, v, gr[lo:hi], lp[lo:hi], step, group["lr"], b1, b2,
                                               group["eps"], group["weight_decay"], bc, adamw, grad_scale)
 
                 self.nvme_swapper.step(og, upd)
@@ -912,7 +937,7 @@ class FlatZeroOptimizer:
             if x0 < x1:
                 dst = fetch(og, on_host)
                 if dst is not None:
-                    dst[moff + x0 - lo:moff + x1 - lo].copy_(flat[x0 - a:x1 - a])
+                    _flat_write(dst, moff + x0 - lo, flat[x0 - a:x1 - a])
                 if also_shard:
                     g.shard[x0 - g.seg_lo:x1 - g.seg_lo].copy_(flat[x0 - a:x1 - a])
 
@@ -1030,7 +1055,8 @@ class FlatZeroOptimizer:
         sd[CK.PARTITION_COUNT] = self.partition_count()
         sd[CK.BASE_OPTIMIZER_STATE] = self.optimizer.state_dict()
         sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS] = [m.detach().cpu() for m in self.master]
-        sd["fp32_host_partitions"] = [m.detach().clone() if m is not None else None for m in self.master_host]
+        sd["fp32_host_partitions"] = [None if m is None else (m.read_full() if hasattr(m, "read_full") else
+                                                              m.detach().clone()) for m in self.master_host]
         sd["host_optimizer_states"] = {og: [s[0].clone(), s[1].clone(), s[2]] for og, s in self.host_states.items()}
         if self.nvme_swapper is not None:
             for og in self.nvme_swapper.sizes:
@@ -1089,8 +1115,15 @@ class FlatZeroOptimizer:
         """Re-read master weights from the (possibly externally modified) bf16 shards."""
         for g in self.groups:
             for (s, e, og, moff, on_host) in g.runs:
-                dst = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
-                dst.copy_(g.shard[s:e].float())
+                _flat_write((self.master_host if on_host else self.master)[og], moff, g.shard[s:e].float())
+
+
+def _flat_write(dst, lo, t):
+    """dst[lo:lo + n] = t for a flat fp32 tensor or an NVMe-resident master (`NvmeFlat`)."""
+    if hasattr(dst, "write"):
+        dst.write(lo, t)
+    else:
+        dst[lo:lo + t.numel()].copy_(t)
 
 
 class _nullctx:

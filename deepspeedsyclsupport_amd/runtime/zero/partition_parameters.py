@@ -1,11 +1,21 @@
 """`zero.Init` (construct a model already partitioned) and `GatheredParameters` (temporarily materialise partitioned
 params), reference `runtime/zero/partition_parameters.py:303-2134`.
 
-Init: while active, every nn.Module's `__init__` is post-processed: its freshly created parameters are moved to the
-GPU, cast to the training dtype, made identical across ranks (broadcast from rank 0, as the reference does at
-`:423`) and reduced to this rank's 1/dp slice `p.ds_tensor`; `p.data` becomes empty. The model never exists in full
-on any GPU, so a 70B model can be built on a node whose per-GPU memory only holds its shard. `DeepSpeedEngine` then
-regroups these per-parameter shards into its flat groups one parameter at a time.
+Init: while active, tensors are created on the accelerator (the default device is switched, the reference patches
+the tensor constructors for the same effect, `:373-555`), and every nn.Module's `__init__` is post-processed: its
+freshly created parameters are cast to the training dtype, made identical across ranks (broadcast from rank 0, as
+the reference does at `:423`) and reduced to this rank's 1/dp slice `p.ds_tensor`; `p.data` becomes empty. At most
+one module's parameters exist in full at any time (never on the host), so a 70B model can be built on a node whose
+per-GPU memory only holds its shard. `DeepSpeedEngine` then regroups these per-parameter shards into its flat
+groups one parameter at a time.
+
+Per-parameter API (reference `:1336-1338` `all_gather` / `partition` + `ds_*` attributes): every partitioned param
+carries `ds_shape`, `ds_numel`, `ds_status` and the methods `p.all_gather(param_list=None)` / `p.partition(
+param_list=None)` (materialise / drop outside a `GatheredParameters` block).
+
+`register_external_parameter(module, param)`: `module`'s forward uses a parameter owned by another module (tied
+embeddings, shared projections). Under ZeRO-3 the fetch hooks of `module` then gather that parameter's group too
+(reference `partition_parameters.py` register_external_parameter + `parameter_offload.py` external params).
 """
 import functools
 
@@ -24,13 +34,63 @@ def _ceil(a, b):
     return (a + b - 1) // b
 
 
+_active_inits = []
+
+
 def shutdown_init_context():
-    """Called by `initialize()` (reference `partition_parameters.py:shutdown_init_context`)."""
-    return None
+    """Suspend an active `zero.Init` (reference `partition_parameters.py:shutdown_init_context`, called by
+    `initialize()` so modules the engine builds internally are not partitioned)."""
+    for ctx in _active_inits:
+        ctx._suspend()
 
 
 def restore_init_context():
+    for ctx in _active_inits:
+        ctx._resume()
+
+
+# ------------------------------------------------------------------------------------------------ per-param API
+def _param_all_gather(p, param_list=None, async_op=False):
+    params = [p] if param_list is None else list(param_list)
+    ctx = GatheredParameters(params)
+    ctx.__enter__()
+    for q in ctx.params:
+        q.__dict__["_ds_gather_ctx"] = ctx
     return None
+
+
+def _param_partition(p, param_list=None, has_been_updated=False):
+    params = [p] if param_list is None else list(param_list)
+    done = set()
+    for q in params:
+        ctx = q.__dict__.pop("_ds_gather_ctx", None)
+        if ctx is not None and id(ctx) not in done:
+            done.add(id(ctx))
+            ctx.__exit__(None, None, None)
+
+
+def _attach_api(p):
+    p.all_gather = functools.partial(_param_all_gather, p)
+    p.partition = functools.partial(_param_partition, p)
+
+
+# ------------------------------------------------------------------------------------------------ external params
+def register_external_parameter(module, parameter):
+    """Declare that `module`'s forward uses `parameter` although another module owns it."""
+    if not isinstance(parameter, nn.Parameter):
+        raise RuntimeError("register_external_parameter: parameter must be a torch.nn.Parameter")
+    ext = module.__dict__.setdefault("_ds_external_params", [])
+    if all(q is not parameter for q in ext):
+        ext.append(parameter)
+    g = getattr(parameter, "ds_group", None)
+    coord = getattr(getattr(g, "_opt", None), "coordinator", None) if g is not None else None
+    if coord is not None:
+        coord.install_external(module)
+
+
+def unregister_external_parameter(module, parameter):
+    ext = module.__dict__.get("_ds_external_params", [])
+    module.__dict__["_ds_external_params"] = [q for q in ext if q is not parameter]
 
 
 def is_zero_param(p):
@@ -54,6 +114,7 @@ def _partition_param(p, dp, rank, group, device, dtype):
     p.ds_status = ZeroParamStatus.NOT_AVAILABLE
     p.ds_process_group = group
     p.data = torch.empty(0, dtype=data.dtype, device=device)
+    _attach_api(p)
 
 
 @torch.no_grad()
@@ -106,11 +167,28 @@ class Init:
             for p in m.parameters(recurse=False):
                 _partition_param(p, self.dp, self.rank, self.group, self.device, self.dtype)
 
+    def _suspend(self):
+        self._suspended = True
+        if getattr(self, "_prev_device", None) is not None:
+            torch.set_default_device(self._prev_device)
+
+    def _resume(self):
+        self._suspended = False
+        if getattr(self, "_prev_device", None) is not None:
+            torch.set_default_device(self.device)
+
     def __enter__(self):
         global _init_depth
         if not self.enabled:
             return self
         _init_depth += 1
+        self._suspended = False
+        _active_inits.append(self)
+        # born on the accelerator: module constructors allocate straight into device memory
+        self._prev_device = None
+        if self.device.type != "cpu":
+            self._prev_device = torch.get_default_device()
+            torch.set_default_device(self.device)
         self._orig_init = nn.Module.__init__
         ctx = self
         orig = self._orig_init
@@ -126,6 +204,8 @@ class Init:
             @functools.wraps(init)
             def wrapped(module, *a, **k):
                 init(module, *a, **k)
+                if ctx._suspended:
+                    return
                 for p in module.parameters(recurse=False):
                     _partition_param(p, ctx.dp, ctx.rank, ctx.group, ctx.device, ctx.dtype)
 
@@ -159,6 +239,10 @@ class Init:
             return False
         for cls, init in self._patched.items():
             cls.__init__ = init
+        if self._prev_device is not None:
+            torch.set_default_device(self._prev_device)
+        if self in _active_inits:
+            _active_inits.remove(self)
         if self._had_init_subclass:
             nn.Module.__init_subclass__ = self._orig_init_subclass
         else:

@@ -1,6 +1,7 @@
 """ZeRO-Offload / Twin-Flow / ZeRO-Infinity optimizer offload (reference `tests/unit/runtime/zero/test_zero.py`
 offload cases, `test_zeropp`/`test_nvme_checkpointing`): host-stepped partitions (native CPU Adam, optionally with
-moments streamed from NVMe files) must reproduce the all-device run, and checkpoints must round-trip."""
+the fp32 master and moments streamed from NVMe files) must reproduce the all-device run, and checkpoints must
+round-trip."""
 import pytest
 import torch
 
@@ -16,10 +17,17 @@ def _run(offload, out, nvme_dir, ckpt_dir):
     if offload is not None:
         device, ratio = offload
         cfg["zero_optimization"]["offload_optimizer"] = {"device": device, "ratio": ratio, "nvme_path": nvme_dir}
+        if device == "nvme":
+            cfg["zero_optimization"]["sub_group_size"] = 5000  # several chunks through the read-ahead pipeline
     eng, _, _, _ = ds.initialize(model=tiny_llama(), config=cfg)
     if offload and offload[0] == "nvme":
-        assert eng.optimizer.nvme_swapper is not None
-        eng.optimizer.nvme_swapper.chunk = 5000  # force several chunks through the read-ahead pipeline
+        from deepspeedsyclsupport_amd.runtime.swap_tensor.optimizer_swapper import NvmeFlat
+        sw = eng.optimizer.nvme_swapper
+        assert sw is not None and sw.chunk == 5000 and sw.with_master
+        # the fp32 master of the host partition is NVMe-resident, not a DRAM tensor
+        assert all(isinstance(m, NvmeFlat) for m in eng.optimizer.master_host if m is not None)
+        if offload[1] == 1.0:
+            assert any(m is not None for m in eng.optimizer.master_host)
     losses = []
     for x in random_tokens(3, 2, 16, seed=40 + dist.get_rank()):
         loss = eng(x, labels=x)
