@@ -556,12 +556,14 @@ void register_inference_ops(pybind11::module& m);  // bind/infer_bind.cpp
 void register_host_mem_ops(pybind11::module& m);   // bind/host_mem.cpp
 void register_comm_ops(pybind11::module& m);       // bind/comm_bind.cpp
 void register_moe_ops(pybind11::module& m);        // bind/moe_bind.cpp
+void register_attn_small_ops(pybind11::module& m); // bind/attn_small_bind.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_inference_ops(m);
   register_host_mem_ops(m);
   register_comm_ops(m);
   register_moe_ops(m);
+  register_attn_small_ops(m);
   m.doc() = "deepspeedsyclsupport_amd gfx950 kernels";
   m.def("adam_flat", &adam_flat);
   m.def("adam_multi", &adam_multi);

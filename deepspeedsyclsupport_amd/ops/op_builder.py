@@ -43,6 +43,7 @@ EXTENSIONS = {
             "attn/flash_fwd.hip",
             "attn/flash_bwd.hip",
             "attn/paged_prefill.hip",
+            "attn/flash_small.hip",
             "quant/quant_kernels.hip",
             "gemv/skinny_gemm.hip",
             "gemv/skinny_mfma.hip",
@@ -51,7 +52,7 @@ EXTENSIONS = {
             "comm/xgmi_allreduce.hip",
         ],
         "bindings": ["bind/ds_hip_ops.cpp", "bind/infer_bind.cpp", "bind/moe_bind.cpp", "bind/host_mem.cpp",
-                     "bind/comm_bind.cpp"],
+                     "bind/comm_bind.cpp", "bind/attn_small_bind.cpp"],
     },
     # host ops: CPU Adam/Adagrad/Lion (ZeRO-Offload, Twin-Flow), async tensor I/O (ZeRO-Infinity), shm all-reduce
     "ds_cpu_ops": {

@@ -4,8 +4,9 @@ DeepSpeedTransformerConfig and `csrc/transformer/ds_transformer_cuda.cpp:154-300
 Same parameters (attn_qkvw/b, attn_ow/b, attn_nw/b, inter_w/b, output_w/b, norm_w/b) and pre-/post-LN semantics:
   pre-LN : x1 = LN_a(x);  r = x + drop(Attn(x1));  out = r + drop(FF(LN_n(r)))
   post-LN: r = LN_a(x + drop(Attn(x)));  out = LN_n(r + drop(FF(r)))
-The MI355X pipeline: hipBLASLt GEMMs for QKV / O / FF1 / FF2, the fused attention kernel (SDPA with the additive
-BERT mask), gfx950 LayerNorm kernels with the residual add fused in, and the fused bias+GELU kernel; autograd
+The MI355X pipeline: hipBLASLt GEMMs for QKV / O / FF1 / FF2, the fused small-head attention kernel
+(`csrc/attn/flash_small.hip`: per-key additive BERT mask and attention-probability dropout in-kernel, reading Q/K/V
+straight from the QKV GEMM output; SDPA for fp32 / host tensors / other head dims), gfx950 LayerNorm kernels with the residual add fused in, and the fused bias+GELU kernel; autograd
 recomputation options map to activation checkpointing of the GELU output (gelu_checkpoint) and attention dropout
 (attn_dropout_checkpoint).
 """
@@ -18,6 +19,20 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from . import functional as DF
+from .. import flash_small as FS
+
+
+def _per_key_mask(mask, B, S):
+    """The additive BERT mask as [B, S] when it only varies per key ([B, S], [B, 1, 1, S] or [B, 1, S] forms)."""
+    if mask is None:
+        return None
+    if mask.dim() == 2 and tuple(mask.shape) == (B, S):
+        return mask
+    if mask.dim() == 4 and mask.shape[1] == 1 and mask.shape[2] == 1 and mask.shape[3] == S and mask.shape[0] in (1, B):
+        return mask[:, 0, 0, :].expand(B, S)
+    if mask.dim() == 3 and mask.shape[1] == 1 and mask.shape[2] == S and mask.shape[0] in (1, B):
+        return mask[:, 0, :].expand(B, S)
+    return None
 
 
 class TransformerConfig:
@@ -100,13 +115,11 @@ class DeepSpeedTransformerLayer(nn.Module):
             # [q, k, v, o, attn_norm, inter, output, norm] weights / biases (reference order)
             self.attn_qkvw = nn.Parameter(torch.cat([w.data for w in initial_weights[:3]]))
             self.attn_qkvb = nn.Parameter(torch.cat([b.data for b in initial_biases[:3]]))
-            names = ["attn_o", "attn_n", "inter_", "output_", "norm_"]
             self.attn_ow, self.attn_ob = nn.Parameter(initial_weights[3].data), nn.Parameter(initial_biases[3].data)
             self.attn_nw, self.attn_nb = nn.Parameter(initial_weights[4].data), nn.Parameter(initial_biases[4].data)
             self.inter_w, self.inter_b = nn.Parameter(initial_weights[5].data), nn.Parameter(initial_biases[5].data)
             self.output_w, self.output_b = nn.Parameter(initial_weights[6].data), nn.Parameter(initial_biases[6].data)
             self.norm_w, self.norm_b = nn.Parameter(initial_weights[7].data), nn.Parameter(initial_biases[7].data)
-            del names
 
     def init_transformer_weights(self, adjust_init_range=False):
         std = self.config.initializer_range
@@ -132,8 +145,15 @@ class DeepSpeedTransformerLayer(nn.Module):
         B, S, H = x.shape
         nh = self.config.heads
         qkv = F.linear(x, self.attn_qkvw, self.attn_qkvb).view(B, S, 3, nh, H // nh)
-        q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
         p = self.config.attn_dropout_ratio if self.training else 0.0
+        key_mask = _per_key_mask(mask, B, S)
+        if FS.supported(qkv) and (mask is None or key_mask is not None):
+            # fused kernel: [B, S, nh, D] views of the QKV GEMM output, per-key mask and attention dropout in-kernel
+            q, k, v = qkv.unbind(2)
+            b1 = key_mask.to(qkv.dtype) if key_mask is not None else None
+            ctx = FS.flash_small(q, k, v, b1, dropout_p=p)
+            return F.linear(ctx.view(B, S, H), self.attn_ow)
+        q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
         if mask is not None:
             mask = mask.to(q.dtype)
             if mask.dim() == 2:
