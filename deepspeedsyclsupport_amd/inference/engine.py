@@ -68,6 +68,14 @@ class InferenceEngine(torch.nn.Module):
         self.injected = False
         self.encoder_injected = 0
         from ..module_inject import encoder as enc
+        if not isinstance(model, torch.nn.Module):
+            # diffusers-style pipeline (reference engine.py: generic_injection for non-Module models)
+            from ..module_inject.replace_module import generic_injection
+            dt = self.dtype if self.dtype in (torch.float16, torch.bfloat16) else None
+            self.module = generic_injection(model, dtype=dt, enable_cuda_graph=config.enable_cuda_graph)
+            self.pipeline_injected = True  # forward() calls the pipeline itself
+            log_dist("InferenceEngine: diffusers pipeline injected (UNet / VAE / text encoder)", ranks=[0])
+            return
         if config.replace_with_kernel_inject and not convert.supported(model) and enc.supported(model):
             # bidirectional encoders (BERT family): fused layers swapped in place, HF embeddings / heads kept
             dt = self.dtype if self.dtype in (torch.float16, torch.bfloat16, torch.float32) else torch.bfloat16

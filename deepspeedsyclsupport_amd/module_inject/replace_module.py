@@ -54,5 +54,12 @@ def revert_transformer_layer(orig_layer_impl, model, config, preln=False):
 
 
 def generic_injection(module, dtype=None, enable_cuda_graph=True):
-    """Diffusers-style injection (UNet/VAE/CLIP) is served by the fused attention + norm ops directly."""
+    """Diffusers pipeline injection (reference `replace_module.py:generic_injection`): for a pipeline object, the
+    UNet / VAE attention modules and transformer blocks are replaced by the fused MI355X modules and the UNet / VAE /
+    text encoder are wrapped in HIP-graph replaying wrappers (`module_inject/diffusers.py`). A plain `nn.Module` is
+    returned unchanged (as in the reference, which only injects pipelines here)."""
+    if isinstance(module, torch.nn.Module):
+        return module
+    from .diffusers import inject_pipeline
+    inject_pipeline(module, dtype=dtype, enable_cuda_graph=enable_cuda_graph)
     return module

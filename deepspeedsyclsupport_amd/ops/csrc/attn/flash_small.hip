@@ -84,8 +84,9 @@ struct SmallArgs {
   float pdrop;     // 0 = no dropout
   uint32_t thresh; // keep if philox >= thresh
   uint64_t seed;
-  int vec_bias;    // biases 8-B aligned with S % 4 == 0: one 4-key load per group
+  int vec_bias;    // bias rows in whole 16-B chunks (Sk % 8 == 0, 16-B aligned rows): one load per 8 keys
   int nsplit;      // dB2 pass: the b2_div sharing z are split over this many workgroups (atomics when > 1)
+  int Sk;          // keys (the forward may attend to a context of another length; the backward needs Sk == S)
 };
 
 // 4 consecutive 16-bit values (8-B aligned) added to f as fp32 / stored from fp32
@@ -155,7 +156,7 @@ struct KeyTile {
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int c = tid + i * NTHR, row = c / CPR, ch = c % CPR;
-        const int key = min(k0 + row, a.S - 1);
+        const int key = min(k0 + row, a.Sk - 1);
         rk[i] = *reinterpret_cast<const u32x4_t*>(Kp + (int64_t)key * a.ks + ch * 8);
         rv[i] = *reinterpret_cast<const u32x4_t*>(Vp + (int64_t)key * a.vs + ch * 8);
       }
@@ -165,10 +166,10 @@ struct KeyTile {
       for (int i = 0; i < 4; ++i) {
         const int c = tid + i * NTHR, row = c >> 3, ch = c & 7;
         const int q = min(qrow0 + row, a.S - 1);
-        rb2[i] = bias_chunk(b2blk + (int64_t)q * a.S, k0 + ch * 8, a.S, a.vec_bias);
+        rb2[i] = bias_chunk(b2blk + (int64_t)q * a.Sk, k0 + ch * 8, a.Sk, a.vec_bias);
       }
     }
-    if (b1p && tid < BN / 8) rb1 = bias_chunk(b1p, k0 + tid * 8, a.S, a.vec_bias);
+    if (b1p && tid < BN / 8) rb1 = bias_chunk(b1p, k0 + tid * 8, a.Sk, a.vec_bias);
   }
   __device__ __forceinline__ void store(char* buf, int tid, bool hb1, bool hb2, bool kv = true) {
     if (kv) {
@@ -228,7 +229,7 @@ __global__ void __launch_bounds__(NTHR, 2) small_fwd_kernel(SmallArgs<T> a) {
   const T* Kp = a.k + z * a.kz + hd * a.kh;
   const T* Vp = a.v + z * a.vz + hd * a.vh;
   const T* b1p = a.b1 ? a.b1 + z * a.b1_zs : nullptr;
-  const T* b2blk = a.b2 ? a.b2 + ((int64_t)(z / a.b2_div) * a.H + hd) * a.S * a.S : nullptr;
+  const T* b2blk = a.b2 ? a.b2 + ((int64_t)(z / a.b2_div) * a.H + hd) * a.S * a.Sk : nullptr;
   const bool hb1 = b1p != nullptr, hb2 = b2blk != nullptr;
   const uint64_t drow = ((uint64_t)z * a.H + hd) * (uint64_t)a.S + (uint64_t)qrow;
 
@@ -247,7 +248,7 @@ __global__ void __launch_bounds__(NTHR, 2) small_fwd_kernel(SmallArgs<T> a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
-  const int nt = (a.S + BN - 1) / BN;
+  const int nt = (a.Sk + BN - 1) / BN;
   const float LOG2E = 1.4426950408889634f;
   const float inv_keep = a.pdrop > 0.f ? 1.f / (1.f - a.pdrop) : 1.f;
   const int gch = (lane >> 1) & 1, colhalf = (lane >> 4) & 1;
@@ -278,7 +279,7 @@ __global__ void __launch_bounds__(NTHR, 2) small_fwd_kernel(SmallArgs<T> a) {
       for (int g = 0; g < 4; ++g) {
         const int kr = t * 32 + 8 * g + 4 * h;
         float bb[4];
-        tile_bias4<T, D>(buf, buf, hb1, hb2, wid * 32 + l32, kr, k0 + kr, a.S, bb);
+        tile_bias4<T, D>(buf, buf, hb1, hb2, wid * 32 + l32, kr, k0 + kr, a.Sk, bb);
 #pragma unroll
         for (int i = 0; i < 4; ++i) s[t][4 * g + i] = s[t][4 * g + i] * a.scale + bb[i];
       }
@@ -873,16 +874,16 @@ int dispatch_small(SmallArgs<T> a, int D, bool bwd, hipStream_t st) {
 
 // Forward. strides[12] = (q z,s,h)(k)(v)(o); dtype DS_BF16 / DS_F16; b1 / b2 may be null.
 extern "C" int ds_flash_small_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const void* b1,
-                                  const void* b2, const int64_t* st, int64_t b1_zs, int Z, int H, int S, int D,
+                                  const void* b2, const int64_t* st, int64_t b1_zs, int Z, int H, int S, int Sk, int D,
                                   int b2_div, float scale, float pdrop, uint64_t seed, int vec_bias, int dtype,
                                   hipStream_t stream) {
-  if (Z <= 0 || H <= 0 || S <= 0 || b2_div <= 0 || (D != 32 && D != 64) || pdrop < 0.f || pdrop >= 1.f)
+  if (Z <= 0 || H <= 0 || S <= 0 || Sk <= 0 || b2_div <= 0 || (D != 32 && D != 64) || pdrop < 0.f || pdrop >= 1.f)
     return (int)hipErrorInvalidValue;
   const uint32_t thresh = (uint32_t)fminf(4294967295.f, pdrop * 4294967296.f);
 #define DS_SMALL_ARGS(T)                                                                                        \
   SmallArgs<T> a{(const T*)q, (const T*)k, (const T*)v, nullptr, nullptr, (T*)o, lse, (const T*)b1, (const T*)b2, \
                  nullptr, nullptr, nullptr, nullptr, nullptr, st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7],     \
-                 st[8], st[9], st[10], st[11], 0, 0, 0, 0, 0, 0, b1_zs, Z, H, S, b2_div, scale, pdrop, thresh, seed, vec_bias, 1};
+                 st[8], st[9], st[10], st[11], 0, 0, 0, 0, 0, 0, b1_zs, Z, H, S, b2_div, scale, pdrop, thresh, seed, vec_bias, 1, Sk};
   if (dtype == DS_BF16) {
     DS_SMALL_ARGS(bf16)
     return dispatch_small<bf16>(a, D, false, stream);
@@ -909,7 +910,7 @@ extern "C" int ds_flash_small_bwd(const void* q, const void* k, const void* v, c
   SmallArgs<T> a{(const T*)q, (const T*)k, (const T*)v, (const T*)o, (const T*)dout, (T*)dq, (float*)lse,           \
                  (const T*)b1, (const T*)b2, (T*)dk, (T*)dv, delta, db1, db2, st[0], st[1], st[2], st[3], st[4], st[5], st[6],      \
                  st[7], st[8], st[9], st[10], st[11], st[12], st[13], st[14], st[15], st[16], st[17], b1_zs, Z, H, S, b2_div, scale, pdrop, \
-                 thresh, seed, vec_bias, 1};
+                 thresh, seed, vec_bias, 1, S};
   if (dtype == DS_BF16) {
     DS_SMALL_ARGS(bf16)
     return dispatch_small<bf16>(a, D, true, stream);

@@ -40,6 +40,8 @@ class FlashSmallFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, b1, b2, b2_div, scale, pdrop, seed):
         from .native import hip_ops
+        if q.shape[1] != k.shape[1] and any(ctx.needs_input_grad[:5]):
+            raise NotImplementedError("flash_small: the backward needs the same query and key length")
         q, k, v = _fix(q), _fix(k), _fix(v)
         o, lse = hip_ops().flash_small_fwd(q, k, v, b1, b2, int(b2_div), float(scale), float(pdrop), int(seed))
         ctx.save_for_backward(q, k, v, o, lse, b1, b2)
@@ -60,7 +62,8 @@ class FlashSmallFunc(torch.autograd.Function):
 
 
 def flash_small(q, k, v, bias1=None, bias2=None, b2_div=1, scale=None, dropout_p=0.0, seed=None):
-    """q/k/v [Z, S, H, D] -> o [Z, S, H, D] (contiguous). bias1 [Z, S], bias2 [Z / b2_div, H, S, S] (q dtype)."""
+    """q [Z, S, H, D], k/v [Z, Sk, H, D] -> o [Z, S, H, D] (contiguous). bias1 [Z, Sk], bias2 [Z / b2_div, H, S, Sk]
+    (q dtype). Sk != S (cross-attention) is forward-only."""
     scale = q.shape[-1]**-0.5 if scale is None else scale
     if dropout_p > 0.0 and seed is None:
         seed = new_seed()

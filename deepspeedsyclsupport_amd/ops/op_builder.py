@@ -242,13 +242,83 @@ _BUILDERS = {
     "RandomLTDBuilder": ("random_ltd", "ds_hip_ops"),
     "SpatialInferenceBuilder": ("spatial_inference", "ds_hip_ops"),
     "SparseAttnBuilder": ("sparse_attn", "ds_hip_ops"),
-    "EvoformerAttnBuilder": ("evoformer_attn", "ds_hip_ops"),
-    "InferenceCutlassBuilder": ("cutlass_ops", "ds_hip_ops"),
     "RaggedUtilsBuilder": ("ragged_ops", "ds_hip_ops"),
 }
 for _cls, (_name, _ext) in _BUILDERS.items():
     globals()[_cls] = _mk(_cls, _name, _ext)
 
+
+
+class EvoformerAttnBuilder(OpBuilder):
+    """Reference `op_builder/evoformer_attn.py` (CUTLASS fMHA): `load()` gives `attention(Q, K, V, bias1, bias2, O,
+    lse)` / `attention_bwd(dO, Q, K, V, O, lse, delta, bias1, bias2, dQ, dK, dV, dB1, dB2)` with the reference's
+    in-place contract, served by `csrc/attn/flash_small.hip` (head dim 32 / 64, bf16 / fp16)."""
+    NAME = "evoformer_attn"
+    EXT = "ds_hip_ops"
+
+    def load(self, verbose=False):
+        import types
+
+        from . import flash_small as FS
+        ext = load(self.EXT)
+
+        def _shape(Q):
+            *lead, S, H, D = Q.shape
+            n = 1
+            for d in lead:
+                n *= d
+            return n, S, H, D, (lead[1] if len(lead) >= 2 else 1)
+
+        def attention(Q, K, V, bias1, bias2, O, lse):
+            Z, S, H, D, N = _shape(Q)
+            b1 = bias1.reshape(Z, S) if bias1.numel() else None
+            b2 = bias2.reshape(Z // N, H, S, S) if bias2.numel() else None
+            o, l = ext.flash_small_fwd(FS._fix(Q.reshape(Z, S, H, D)), FS._fix(K.reshape(Z, S, H, D)),
+                                       FS._fix(V.reshape(Z, S, H, D)), b1, b2, N, D**-0.5, 0.0, 0)
+            O.copy_(o.view_as(O))
+            lse.view(Z, H, -1)[..., :S].copy_(l.view(Z, H, S))  # reference lse rows are padded to 32
+
+        def attention_bwd(dO, Q, K, V, O, lse, delta, bias1, bias2, dQ, dK, dV, dB1, dB2):
+            Z, S, H, D, N = _shape(Q)
+            b1 = bias1.reshape(Z, S) if bias1.numel() else None
+            b2 = bias2.reshape(Z // N, H, S, S) if bias2.numel() else None
+            l = lse.reshape(Z, H, -1)[..., :S].contiguous()
+            r = ext.flash_small_bwd(FS._fix(dO.reshape(Z, S, H, D)), FS._fix(Q.reshape(Z, S, H, D)),
+                                    FS._fix(K.reshape(Z, S, H, D)), FS._fix(V.reshape(Z, S, H, D)),
+                                    FS._fix(O.reshape(Z, S, H, D)), l, b1, b2, N, D**-0.5, 0.0, 0,
+                                    dB1.numel() > 0, dB2.numel() > 0)
+            for dst, src in zip((dQ, dK, dV), r[:3]):
+                dst.copy_(src.view_as(dst))
+            if dB1.numel():
+                dB1.copy_(r[3].view_as(dB1))
+            if dB2.numel():
+                dB2.copy_(r[4].view_as(dB2))
+
+        return types.SimpleNamespace(attention=attention, attention_bwd=attention_bwd)
+
+    jit_load = load
+
+
+class InferenceCutlassBuilder(OpBuilder):
+    """Reference `op_builder/inference_cutlass_builder.py` (CUTLASS `mixed_gemm` / `moe_gemm`): `load()` gives the
+    same entry points on the MI355X int8 kernels (`ops/cutlass_ops.py`). int8 weights run natively (pre-shuffled
+    MFMA stream / dequant + library GEMM); int4 weights are unpacked to int8 at first use — there is no native int4
+    kernel, so `is_compatible(num_bits=4)` says False."""
+    NAME = "cutlass_ops"
+    EXT = "ds_hip_ops"
+
+    def is_compatible(self, verbose=False, num_bits=8):
+        return num_bits == 8 and super().is_compatible(verbose)
+
+    def load(self, verbose=False):
+        import types
+
+        from . import cutlass_ops as C
+        load(self.EXT)
+        return types.SimpleNamespace(mixed_gemm=C.mixed_gemm, moe_gemm=C.moe_gemm, MixedGEMM=C.MixedGEMM,
+                                     MoEGEMM=C.MoEGEMM, MixedMoEGEMM=C.MixedMoEGEMM)
+
+    jit_load = load
 
 
 class UtilsBuilder(OpBuilder):
@@ -268,4 +338,5 @@ class UtilsBuilder(OpBuilder):
 
 
 ALL_OPS = {globals()[c].NAME: globals()[c] for c in _BUILDERS}
-ALL_OPS["utils"] = UtilsBuilder
+for _b in (UtilsBuilder, EvoformerAttnBuilder, InferenceCutlassBuilder):
+    ALL_OPS[_b.NAME] = _b

@@ -1,0 +1,94 @@
+"""Mixed-precision GEMM entry points of `InferenceCutlassBuilder` (reference
+`inference/v2/kernels/cutlass_ops/mixed_gemm/mixed_gemm.py`, `moe_gemm/moe_gemm.py`) against fp32 dequantised
+references; the GPU variant runs the pre-shuffled int8 kernels."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deepspeedsyclsupport_amd.ops import cutlass_ops as C
+from deepspeedsyclsupport_amd.ops.op_builder import ALL_OPS, InferenceCutlassBuilder
+
+
+def _quant(w, bits):
+    qmax = 2**(bits - 1) - 1
+    s = w.abs().amax(0).clamp_min(1e-8) / qmax          # per output channel (w is [in, out])
+    q = torch.round(w / s).clamp(-qmax - 1, qmax).to(torch.int8)
+    return q, s
+
+
+def test_int4_pack_roundtrip():
+    q = torch.randint(-8, 8, (64, 32), dtype=torch.int8)
+    assert torch.equal(C.unpack_int4(C.pack_int4(q)), q)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+@pytest.mark.parametrize("rows", [3, 40])
+def test_mixed_gemm_cpu(bits, rows):
+    torch.manual_seed(0)
+    K, N = 128, 96
+    w = torch.randn(K, N)
+    q, s = _quant(w, bits)
+    x = torch.randn(rows, K)
+    b = torch.randn(N)
+    weights = C.pack_int4(q) if bits == 4 else q
+    out = torch.empty(rows, N, dtype=torch.bfloat16)
+    C.MixedGEMM(torch.bfloat16, "gelu", bits)(out, x.bfloat16(), weights, s, b)
+    ref = F.gelu(x.bfloat16().float() @ (q.float() * s) + b)
+    assert ((out.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
+def test_moe_gemm_cpu():
+    torch.manual_seed(0)
+    E, K, N = 3, 64, 32
+    w = torch.randn(E, K, N)
+    counts = torch.tensor([2, 0, 5])
+    x = torch.randn(int(counts.sum()), K)
+    out = torch.empty(x.shape[0], N)
+    C.MoEGEMM(torch.float32, "relu")(out, x, w, counts.cumsum(0))
+    ref = torch.cat([F.relu(x[:2] @ w[0]), F.relu(x[2:] @ w[2])])
+    torch.testing.assert_close(out, ref)
+
+
+def test_builder_is_honest():
+    b = InferenceCutlassBuilder()
+    assert not b.is_compatible(num_bits=4)
+    assert "cutlass_ops" in ALL_OPS and "evoformer_attn" in ALL_OPS
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 8, 16, 64])
+def test_mixed_gemm_gpu_int8(rows):
+    torch.manual_seed(0)
+    K, N = 512, 384
+    w = torch.randn(K, N, device="cuda")
+    q, s = _quant(w, 8)
+    x = torch.randn(rows, K, device="cuda").bfloat16()
+    out = torch.empty(rows, N, device="cuda", dtype=torch.bfloat16)
+    mod = InferenceCutlassBuilder().load()
+    mod.mixed_gemm(out, x, q, s, None, num_bits=8)
+    ref = x.float() @ (q.float() * s)
+    assert ((out.float() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+
+
+@pytest.mark.gpu
+def test_evoformer_builder_entry_points():
+    from deepspeedsyclsupport_amd.ops.op_builder import EvoformerAttnBuilder
+    from deepspeedsyclsupport_amd.ops import flash_small as FS
+    B, N, S, H, D = 1, 2, 64, 2, 32
+    g = torch.Generator(device="cuda").manual_seed(0)
+    Q, K, V = (torch.randn(B, N, S, H, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    b1 = torch.randn(B, N, 1, 1, S, device="cuda", generator=g).bfloat16()
+    b2 = torch.randn(B, 1, H, S, S, device="cuda", generator=g).bfloat16()
+    k = EvoformerAttnBuilder().load()
+    O = torch.empty_like(Q)
+    lse = torch.empty(B * N, H, 64, device="cuda")
+    k.attention(Q, K, V, b1, b2, O, lse)
+    ref = FS.reference(Q.reshape(B * N, S, H, D), K.reshape(B * N, S, H, D), V.reshape(B * N, S, H, D),
+                       b1.reshape(B * N, S), b2.reshape(B, H, S, S), b2_div=N)
+    assert ((O.reshape(B * N, S, H, D).float() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+    dO = torch.randn_like(O)
+    dQ, dK, dV = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)
+    dB1 = torch.zeros_like(b1, dtype=torch.float32)
+    dB2 = torch.zeros_like(b2, dtype=torch.float32)
+    k.attention_bwd(dO, Q, K, V, O, lse, torch.empty_like(lse), b1, b2, dQ, dK, dV, dB1, dB2)
+    assert torch.isfinite(dQ.float()).all() and dB2.abs().sum() > 0 and dB1.abs().sum() > 0

@@ -120,3 +120,19 @@ def test_bert_layer_uses_kernel_with_mask():
     ref_layer.load_state_dict({k: v.float() for k, v in layer.state_dict().items()})
     ref = ref_layer(x.float(), m)
     assert _rel(out, ref) < 3e-2
+
+
+@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("Sk", [77, 64, 300])
+def test_cross_length_forward(D, Sk):
+    """Queries and keys of different lengths (diffusers cross-attention): forward only, with a per-key bias."""
+    Z, S, H = 2, 150, 2
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q = torch.randn(Z, S, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
+    k, v = (torch.randn(Z, Sk, H, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(2))
+    b1 = torch.randn(Z, Sk, device="cuda", generator=g).bfloat16()
+    with torch.no_grad():
+        out = FS.flash_small(q, k, v, b1)
+    assert _rel(out, FS.reference(q, k, v, b1)) < 2e-2
+    with pytest.raises(NotImplementedError):
+        FS.flash_small(q.requires_grad_(True), k, v)
