@@ -62,6 +62,10 @@ class DeepSpeedZeroConfig(DeepSpeedConfigModel):
     override_module_apply: bool = True
     # debug mode: cross-rank consistency check before every ZeRO collective (runtime/zero/utils.py)
     safe_mode: bool = False
+    # MoE expert-parameter gradient averaging: "global" = mean over the whole data-parallel batch (dense DP size, the
+    # default here); "expert_dp" = mean over the expert-data-parallel group only, i.e. ep_size times larger — the
+    # reference's `stage_1_and_2.py average_tensor` / `engine._reduce_expert_gradients` numerics.
+    moe_expert_grad_scaling: str = "global"
 
     @model_validator(mode="after")
     def _fixups(self):

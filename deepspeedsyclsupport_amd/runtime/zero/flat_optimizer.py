@@ -67,6 +67,7 @@ class FlatGroup:
         self.idx = idx
         self.dp_group = dp_group    # reduction / partition group (DP, or expert-DP for MoE experts)
         self.reduce_dp = dp         # ranks that hold (a partition or a replica of) these params
+        self.expert = False         # MoE expert parameters (set by the optimizer)
         self.params = list(params)
         self.module = module
         self.dtype = dtype
@@ -121,6 +122,9 @@ class FlatZeroOptimizer:
         self.module = module
         self.stage = int(stage)
         self.zc = zero_config
+        self.expert_grad_scaling = str(getattr(zero_config, "moe_expert_grad_scaling", "global") or "global")
+        if self.expert_grad_scaling not in ("global", "expert_dp"):
+            raise ValueError(f"moe_expert_grad_scaling must be 'global' or 'expert_dp', got {self.expert_grad_scaling}")
         self.safe_mode = bool(zero_config is not None and getattr(zero_config, "safe_mode", False))
         self.cfg = ds_config
         self.dtype = dtype
@@ -272,6 +276,7 @@ class FlatZeroOptimizer:
             persistent = d["persistent"] or (not multi and not self.offload_param)
             g = FlatGroup(i, d["params"], gdp, grank, self.stage >= 1 and multi, persistent,
                           self.device, self.dtype, d["module"], dp_group=pg)
+            g.expert = bool(self.optimizer.param_groups[og].get("moe", False))
             self.groups.append(g)
         self.param_group = {}
         import weakref
@@ -497,13 +502,18 @@ class FlatZeroOptimizer:
         f = getattr(self.optimizer, "skip_grad_allreduce", None)
         return bool(f()) if f is not None else False
 
-    def _div(self):
-        # gradient = mean over the GLOBAL batch (dense DP size), for expert groups too; the reference divides expert
-        # grads by the expert-DP size only (an ep-times larger scale, `stage_1_and_2.py` average_tensor)
-        return 1.0 if self._local_grads() else float(self.dp)
+    def _div(self, g=None):
+        # gradient = mean over the GLOBAL batch (dense DP size), for expert groups too by default; with
+        # zero_optimization.moe_expert_grad_scaling = "expert_dp" expert grads are averaged over the expert-DP group
+        # only (an ep-times larger scale: the reference's `stage_1_and_2.py` average_tensor numerics)
+        if self._local_grads():
+            return 1.0
+        if g is not None and g.expert and self.expert_grad_scaling == "expert_dp":
+            return float(g.reduce_dp)
+        return float(self.dp)
 
-    def _prescale(self):
-        return self.comm_dtype == torch.float16 and self._div() > 1
+    def _prescale(self, g=None):
+        return self.comm_dtype == torch.float16 and self._div(g) > 1
 
     @instrument_w_nvtx
     def _reduce_group(self, g):
@@ -521,8 +531,8 @@ class FlatZeroOptimizer:
             self.rs_stream.wait_stream(compute)
         with ctx:
             comm = src if src.dtype == self.comm_dtype else src.to(self.comm_dtype)
-            if self._prescale():
-                comm.mul_(1.0 / self._div())
+            if self._prescale(g):
+                comm.mul_(1.0 / self._div(g))
             if self._local_grads():
                 out = comm  # a communication-compressed optimizer (1-bit Adam/LAMB, 0/1 Adam) averages on its own
             elif g.partition:
@@ -538,7 +548,7 @@ class FlatZeroOptimizer:
                 dist.all_reduce(comm, group=g.dp_group)
                 out = comm[g.seg_lo:g.seg_lo + g.seg]
             if g.mode == self.COPY and self.gas > 1:
-                self._accumulate_runs(g, out, self._alpha())
+                self._accumulate_runs(g, out, self._alpha(g))
             else:
                 g.red_out = out
             if g.mode == self.COPY:
@@ -546,8 +556,8 @@ class FlatZeroOptimizer:
                     src.record_stream(self.rs_stream)
                 g.grad_flat = None
 
-    def _alpha(self):
-        return 1.0 if (self._prescale() or self._div() == 1) else 1.0 / self._div()
+    def _alpha(self, g=None):
+        return 1.0 if (self._prescale(g) or self._div(g) == 1) else 1.0 / self._div(g)
 
     def _accumulate_runs(self, g, seg_grad, alpha):
         first = not g._acc_valid
@@ -655,9 +665,8 @@ class FlatZeroOptimizer:
     def _grad_items(self):
         """[(og, moff, n, grad_1d, lp_1d, scale, on_host)] covering every local master element that has a gradient."""
         items = []
-        alpha = self._alpha()
-        div = self._div()
         for g in self.groups:
+            alpha, div = self._alpha(g), self._div(g)
             for (s, e, og, moff, on_host) in g.runs:
                 if g.mode == self.LOCAL:
                     for i, p in enumerate(g.params):
@@ -1007,12 +1016,12 @@ class FlatZeroOptimizer:
         seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
         if g.mode == self.LOCAL:
             if p.grad is not None:
-                seg32[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1)).mul_(1.0 / self._div())
+                seg32[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1)).mul_(1.0 / self._div(g))
         elif g._acc_valid:
             for (s, e, og, moff, on_host) in g.runs:
                 seg32[s:e].copy_((self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s])
         elif g.red_out is not None:
-            seg32.copy_(g.red_out).mul_(self._alpha())
+            seg32.copy_(g.red_out).mul_(self._alpha(g))
         seg32.mul_(self._unscale_factor())
         if g.partition:
             full = torch.empty(g.padded, dtype=torch.float32, device=self.device)

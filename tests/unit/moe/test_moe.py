@@ -103,3 +103,37 @@ def test_gating_capacity_and_aux_loss():
     assert torch.all(idx2[:, 0] != idx2[:, 1])
     both = (loc2 >= 0).all(1)
     torch.testing.assert_close(w2[both].sum(1), torch.ones(int(both.sum())))
+
+
+def _scaling_run(mode, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    model = MoEModel(ep_size=2)
+    cfg = {"train_micro_batch_size_per_gpu": 6, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}},
+           "zero_optimization": {"stage": 1, "moe_expert_grad_scaling": mode}, "gradient_clipping": 0.0}
+    eng, _, _, _ = ds.initialize(model=model, config=cfg)
+    x, y = _data(dist.get_rank())[0]
+    eng.backward(eng(x, y))
+    grads = {n: eng.optimizer.get_full_grad(p).clone() for n, p in eng.module.named_parameters()}
+    if dist.get_rank() == 0:
+        torch.save(grads, out)
+
+
+def test_moe_expert_grad_scaling_switch(tmp_path):
+    """`moe_expert_grad_scaling`: "global" averages expert grads over the whole DP batch; "expert_dp" over the
+    expert-DP group only (reference numerics) — ep_size = world = 2 gives expert-DP size 1, so a 2x ratio on the
+    expert parameters and identical dense gradients."""
+    got = {}
+    for mode in ("global", "expert_dp"):
+        out = str(tmp_path / f"{mode}.pt")
+        run_distributed(_scaling_run, 2, mode, out)
+        got[mode] = torch.load(out)
+    n_exp = 0
+    for n, g in got["global"].items():
+        h = got["expert_dp"][n]
+        if "deepspeed_experts" in n:
+            torch.testing.assert_close(h, 2 * g)
+            n_exp += 1
+        else:
+            torch.testing.assert_close(h, g)
+    assert n_exp > 0
