@@ -57,8 +57,15 @@ def setup_gemm_tuning(on_gpu):
         tun.tuning_enable(True)
         tun.set_max_tuning_duration(int(os.environ.get("DS_TUNABLEOP_MS", "30")))
         tun.set_max_tuning_iterations(int(os.environ.get("DS_TUNABLEOP_ITERS", "20")))
-        tun.set_filename(TUNED_GEMMS, False)
-        log(f"[bench] TunableOp tuning -> {TUNED_GEMMS}")
+        out = os.environ.get("DS_TUNABLEOP_OUT", TUNED_GEMMS)
+        if out != TUNED_GEMMS and os.path.exists(TUNED_GEMMS):
+            import shutil
+            os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+            shutil.copyfile(TUNED_GEMMS, out)  # keep the recorded shapes; only new ones get tuned
+        tun.set_filename(out, False)
+        if os.path.exists(out):
+            tun.read_file(out)
+        log(f"[bench] TunableOp tuning -> {out}")
         import threading
 
         def heartbeat():  # tuning a step's GEMM shapes takes minutes: keep the job visibly alive

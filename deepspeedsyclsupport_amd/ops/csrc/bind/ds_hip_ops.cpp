@@ -52,6 +52,7 @@ int ds_flash_bwd(const void*, const void*, const void*, const void*, const void*
                  void*, void*, int, int, int, int, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                  const int64_t*, const int64_t*, const int64_t*, const int64_t*, float, int, const int*, const int*,
                  const uint8_t*, int, int, int, int, hipStream_t);
+int ds_transpose16(const void*, void*, int, int, int, int64_t, hipStream_t);
 int ds_xent_fwd(const void*, const int64_t*, float*, float*, int64_t, int, int64_t, int, float, int, hipStream_t);
 int ds_xent_bwd(const void*, const int64_t*, const float*, const float*, float, void*, int64_t, int, int64_t, int64_t,
                 int, float, int, hipStream_t);
@@ -424,6 +425,21 @@ Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, OptT dloss, double dlo
 // ------------------------------------------------------------------------------------------ flash attention
 // q [B,Hq,S,128] / k,v [B,Hk,Skv,128] bf16 views with unit last stride; returns (o [B,Hq,S,128] whose memory is laid
 // out [B,S,Hq,128] so the o_proj GEMM reads it without a transpose copy, lse [B,Hq,S] fp32).
+// x [R, C] (16-bit, unit last stride) -> x^T contiguous [C, Rp] at HBM speed (K-major wgrad GEMM operands);
+// pad_to > R appends zero columns (the contraction dimension rounded up for the GEMM)
+Tensor transpose16(Tensor x, int64_t pad_to) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "transpose16: 2-D device tensor, unit last stride");
+  TORCH_CHECK(x.element_size() == 2, "transpose16: 16-bit dtypes only");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(R % 8 == 0 && C % 8 == 0 && x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "transpose16: sizes / row stride multiples of 8, 16-B aligned base");
+  const int64_t Rp = pad_to > R ? pad_to : R;
+  TORCH_CHECK(Rp % 8 == 0 && Rp < (1LL << 31) && C < (1LL << 31), "transpose16: bad padded size / dims too large");
+  auto out = torch::empty({C, Rp}, x.options());
+  check(ds_transpose16(x.data_ptr(), out.data_ptr(), (int)R, (int)Rp, (int)C, x.stride(0), stream()), "transpose16");
+  return out;
+}
+
 std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale, bool want_lse) {
   TORCH_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "flash_fwd: device tensors expected");
   TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "flash_fwd: 4-D [B,H,S,D] tensors expected");
@@ -587,6 +603,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("hk"), py::arg("rot"), py::arg("pos_offset"), py::arg("token_major") = false);
   m.def("qkv_rope_bwd", &qkv_rope_bwd);
   m.def("rope_inplace", &rope_inplace);
+  m.def("transpose16", &transpose16, py::arg("x"), py::arg("pad_to") = 0);
   m.def("flash_fwd", &flash_fwd);
   m.def("flash_fwd_sparse", &flash_fwd_sparse);
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"),

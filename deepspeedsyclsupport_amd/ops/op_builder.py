@@ -37,6 +37,7 @@ EXTENSIONS = {
             "norm/norm_kernels.hip",
             "act/act_kernels.hip",
             "act/dropout_kernels.hip",
+            "act/transpose.hip",
             "rope/rope_kernels.hip",
             "xent/xent_kernels.hip",
             "attn/decode_attn.hip",

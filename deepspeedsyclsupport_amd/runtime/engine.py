@@ -294,6 +294,12 @@ class DeepSpeedEngine(nn.Module):
         self.basic_optimizer = basic
         stage = self.zero_optimization_stage()
         dtype = self._dtype()
+        zc = self._config.zero_config
+        if getattr(zc, "memory_efficient_linear", True) and next(self.module.parameters()).is_cuda:
+            # every nn.Linear on the training linear of ops/linear.py (K-major weight-gradient GEMMs; the ZeRO-3
+            # coordinator installs the same function for partitioned runs)
+            from .zero.linear import install_zero3_linear
+            install_zero3_linear(self.module)
         self.optimizer = FlatZeroOptimizer(basic, self.module, self._config, dp_group=self.seq_data_parallel_group,
                                            stage=stage, mpu=self.mpu, clip_grad=self.gradient_clipping(),
                                            dtype=dtype,

@@ -7,29 +7,12 @@ backward matmuls read.
 """
 import types
 
-import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
+from ...ops.linear import LinearFunction
 
-class LinearFunctionForZeroStage3(torch.autograd.Function):
-
-    @staticmethod
-    def forward(ctx, x, weight, bias=None):
-        ctx.save_for_backward(x, weight, bias)
-        return F.linear(x, weight, bias)
-
-    @staticmethod
-    def backward(ctx, go):
-        x, weight, bias = ctx.saved_tensors
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = go.matmul(weight)
-        if ctx.needs_input_grad[1]:
-            gw = go.reshape(-1, go.shape[-1]).t().matmul(x.reshape(-1, x.shape[-1]))
-        if bias is not None and ctx.needs_input_grad[2]:
-            gb = go.reshape(-1, go.shape[-1]).sum(0)
-        return gx, gw, gb
+# the training linear of ops/linear.py (saves the Parameter; K-major weight-gradient GEMM for long token dims)
+LinearFunctionForZeroStage3 = LinearFunction
 
 
 def zero3_linear_wrap(input, weight, bias=None):
