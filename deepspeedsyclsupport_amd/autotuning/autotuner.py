@@ -10,7 +10,11 @@ Flow (same contract as the reference):
      user script launched with a derived DeepSpeed config whose engine measures `metric` between
      start_profile_step and end_profile_step and writes it to `metric_path`, then exits;
   4. gridsearch / random / model-based (fit metric ~ mbs per stage, try the predicted best first) ordering with
-     early stopping; the best config is written to `results_dir/ds_config_optimal.json`.
+     early stopping;
+  5. unless `autotuning.fast` (default true), the ZeRO knobs of the winning stage are tuned at its micro-batch size
+     over a tuning space (`autotuning.tuning_space` or `config_templates.DEFAULT_TUNING_SPACE`: bucket sizes,
+     overlap, stage-3 prefetch / live-parameter / persistence budgets) with the `tuner/` grid, random or
+     model-based (surrogate cost model) tuner; the best config is written to `results_dir/ds_config_optimal.json`.
 Experiments are launched through `launcher.runner` (or a caller-supplied `run_experiment` callable, used in tests).
 """
 import copy
@@ -23,6 +27,9 @@ import subprocess
 import sys
 
 from ..utils.logging import logger
+from .config_templates import DEFAULT_TUNING_SPACE
+from .tuner import GridSearchTuner, ModelBasedTuner, RandomTuner
+from .utils import canonical_name, get_all_configs, get_tuning_keys, merge
 
 GB = 1024**3
 
@@ -175,14 +182,16 @@ class Autotuner:
             res = self._run(e)
             val = None if not res else res.get(self.metric)
             self.records.append((e["name"], val))
-            better = val is not None and (best is None or (val < best[1] if self.metric == "latency"
-                                                            else val > best[1]))
-            if better:
+            if self._better(val, best):
                 best, since = (e, val), 0
             else:
                 since += 1
                 if since >= self.early_stop:
                     break
+        if best is not None and not self.at.get("fast", True):
+            tuned = self.tune_space(best[0]["stage"], best[0]["mbs"])
+            if tuned is not None and self._better(tuned[1], best):
+                best = tuned
         self.best = best
         if best is not None:
             out = copy.deepcopy(best[0]["ds_config"])
@@ -193,6 +202,36 @@ class Autotuner:
             json.dump({"records": self.records, "best": best[0]["name"] if best else None,
                        "metric": self.metric, "best_value": best[1] if best else None}, f, indent=2)
         return best
+
+    def _better(self, val, best):
+        return val is not None and (best is None or (val < best[1] if self.metric == "latency" else val > best[1]))
+
+    def tune_space(self, stage, mbs):
+        """Tune the ZeRO knobs of `stage` at micro-batch `mbs` over the tuning space (step 5 above)."""
+        space = copy.deepcopy(self.at.get("tuning_space") or DEFAULT_TUNING_SPACE.get(stage, {}))
+        space.setdefault("zero_optimization", {})["stage"] = stage
+        keys = get_tuning_keys(space)
+        exps = []
+        for point in get_all_configs(space):
+            cfg = merge(self.base, point)
+            cfg["train_micro_batch_size_per_gpu"] = mbs
+            cfg.pop("train_batch_size", None)
+            name = canonical_name(cfg, keys)
+            at = dict(self.at)
+            at.update(enabled=True, metric_path=os.path.join(self.exps_dir, name, "metrics.json"))
+            cfg["autotuning"] = at
+            exps.append({"name": name, "ds_config": cfg, "stage": stage, "mbs": mbs})
+        if len(exps) <= 1:
+            return None
+        if self.tuner_type == "model_based":
+            tuner = ModelBasedTuner(exps, self._run, self.metric, space)
+        elif self.tuner_type == "random":
+            tuner = RandomTuner(exps, self._run, self.metric)
+        else:
+            tuner = GridSearchTuner(exps, self._run, self.metric)
+        tuner.tune(sample_size=1, n_trials=self.num_trials, early_stopping=self.early_stop)
+        self.records += [(e["name"], v) for e, v in tuner.records]
+        return (tuner.best_exp, tuner.best_metric_val) if tuner.best_exp is not None else None
 
     def profile_model_info(self):
         exp = self._exp(0, self.min_mbs)
