@@ -63,13 +63,15 @@ class LinearFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, go):
+        # under autocast the forward GEMM ran in the autocast dtype while x / weight were saved as given: the
+        # backward products run in the gradient's dtype
         x, weight, bias = ctx.saved_tensors
         gx = gw = gb = None
         go2 = go.reshape(-1, go.shape[-1])
         if ctx.needs_input_grad[0]:
-            gx = input_grad(go2, weight).view(*go.shape[:-1], weight.shape[1])
+            gx = input_grad(go2, weight.to(go.dtype)).view(*go.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
-            gw = weight_grad(go2, x.reshape(-1, x.shape[-1]))
+            gw = weight_grad(go2, x.reshape(-1, x.shape[-1]).to(go.dtype))
         if bias is not None and ctx.needs_input_grad[2]:
             gb = go2.sum(0)
         return gx, gw, gb

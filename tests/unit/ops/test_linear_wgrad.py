@@ -47,3 +47,12 @@ def test_kmajor_weight_grad_gpu():
     ref = g.float().t() @ x.float()
     assert ((gw.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
     torch.testing.assert_close(gx.float(), (g.float() @ w.float()), rtol=2e-2, atol=2e-1)
+
+
+def test_linear_function_under_autocast_cpu():
+    lin = torch.nn.Linear(16, 8)
+    x = torch.randn(4, 16, requires_grad=True)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        y = L.linear(x, lin.weight, lin.bias)
+    y.float().sum().backward()
+    assert lin.weight.grad.dtype == torch.float32 and x.grad.dtype == torch.float32
