@@ -127,6 +127,12 @@ class LinearLayer_Compress(nn.Linear):
         self.wq_symmetric = quantization_type == "symmetric"
         self.wq_groups = int(num_groups)
         self.wq_bits = self.wq_start_bits
+        if not weight_quantization_enabled_in_forward:
+            # per-weight MoQ schedule consumed by runtime/quantize.py after each optimizer step (reference
+            # `compression/basic_layer.py:79-84`)
+            self.weight.start_bits = self.wq_start_bits
+            self.weight.target_bits = self.wq_target_bits
+            self.weight.q_period = self.wq_period
 
     def enable_activation_quantization(self, bits, quantization_type, range_calibration):
         self.activation_quantization_enabled = True

@@ -42,6 +42,11 @@ class compression_scheduler:
         self.enabled = set()
         self._step = 0
         self._snip = {}
+        self.moq_external = False  # the engine's MoQ quantizer (runtime/quantize.py) owns the in-place weight quant
+
+    @property
+    def weight_quantization_enabled(self):
+        return any(t == "weight_quantization" for (t, _) in self.enabled)
 
     def _plan(self):
         return getattr(self.model, "_ds_compression_plan", [])
@@ -80,7 +85,7 @@ class compression_scheduler:
                                                                                           False):
                 self._gradual_sparse(m, shared, params, step)
             elif tech == "weight_quantization" and not shared["quantize_weight_in_forward"] and \
-                    getattr(m, "weight_quantization_enabled", False):
+                    getattr(m, "weight_quantization_enabled", False) and not self.moq_external:
                 bits = getattr(m, "wq_bits", getattr(m, "wq_target_bits", 8))
                 with torch.no_grad():
                     m.weight.copy_(fake_quant(m.weight, bits, m.wq_groups, m.wq_symmetric))

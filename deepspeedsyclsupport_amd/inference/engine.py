@@ -64,6 +64,8 @@ class InferenceEngine(torch.nn.Module):
 
         if config.checkpoint is not None and not isinstance(model, torch.nn.Module):
             raise ValueError("init_inference expects an nn.Module (meta-tensor checkpoint loading: pass the model)")
+        if config.checkpoint is not None:
+            self._load_client_checkpoint(model, config)
 
         self.injected = False
         self.encoder_injected = 0
@@ -110,6 +112,25 @@ class InferenceEngine(torch.nn.Module):
         eng.tp_size, eng.tp_rank, eng.mp_group, eng.mpu = tp_size, tp_rank, tp_group, None
         eng.injection_dict = None
         return eng
+
+    def _load_client_checkpoint(self, model, config):
+        """`checkpoint=` JSON / dict (reference `inference/engine.py:400-418,441-503`): HF-layout shard lists
+        (`bloom`, `ds_model`) stream into the (possibly meta-device) client model file by file before injection;
+        Megatron `mp_rank_*` lists are merged / split to this job's tensor-parallel degree and loaded into the
+        client model's module."""
+        from ..runtime.state_dict_factory import AUTO_MODULE_KEY, SDLoaderFactory, load_hf_shards
+        desc = SDLoaderFactory.get_sd_loader_json(config.checkpoint)
+        if isinstance(desc, dict):
+            keys = load_hf_shards(model, desc, base_dir=config.base_dir or "")
+            log_dist(f"InferenceEngine: loaded {len(keys)} tensors from {desc['type']} checkpoint", ranks=[0])
+            return
+        # int8 serving quantises after injection (DSInferenceModel.quantize_weights, pre-shuffled for the int8
+        # kernels), so the checkpoint loads in its stored precision here
+        _, sd, _ = desc.load(self.tp_size, self.tp_rank, module_key=AUTO_MODULE_KEY)
+        module_sd = sd[desc._choose_module_key(sd)]
+        model.load_state_dict(module_sd, strict=False, assign=any(p.is_meta for p in model.parameters()))
+        log_dist(f"InferenceEngine: Megatron checkpoint ({len(desc.ckpt_list)} files) loaded at tp={self.tp_size}",
+                 ranks=[0])
 
     # ------------------------------------------------------------------------------------------ groups
     def _create_model_parallel_group(self, config):

@@ -322,7 +322,15 @@ class DeepSpeedConfig:
         self.curriculum_params_legacy = p.get("curriculum_learning", {})
         self.data_efficiency_config = p.get("data_efficiency", {})
         self.data_efficiency_enabled = self.data_efficiency_config.get("enabled", False)
-        self.eigenvalue_enabled = p.get("eigenvalue", {}).get("enabled", False)
+        ev = p.get("eigenvalue", {})
+        self.eigenvalue_enabled = ev.get("enabled", False)
+        self.eigenvalue_verbose = ev.get("verbose", False)
+        self.eigenvalue_max_iter = ev.get("max_iter", 100)
+        self.eigenvalue_tol = ev.get("tol", 1e-2)
+        self.eigenvalue_stability = ev.get("stability", 1e-6)
+        self.eigenvalue_gas_boundary_resolution = ev.get("gas_boundary_resolution", 1)
+        self.eigenvalue_layer_name = ev.get("layer_name", "bert.encoder.layer")
+        self.eigenvalue_layer_num = ev.get("layer_num", 0)
         ck = CheckpointConfig(**p.get("checkpoint", {}))
         self.checkpoint_config = ck
         self.checkpoint_tag_validation_enabled = ck.tag_validation.lower() != "ignore"

@@ -72,6 +72,17 @@ class Eigenvalue:
 
     @staticmethod
     def post_process(values):
-        """Normalise to (0, 1] by the max (reference semantics); zero stays zero."""
+        """Normalise to (0, 1] by the max; a block with no curvature signal stays 0 here (the per-parameter map
+        below gives it the neutral 1.0, as the reference's `post_process` does)."""
         mx = max(values) if values else 0.0
         return [v / mx if mx > 0 else 0.0 for v in values]
+
+    def compute_block_eigenvalue(self, module, loss=None, device=None, scale=1.0):
+        """{id(param): (normalised eigenvalue, block index)} — the form MoQ consumes (reference
+        `runtime/eigenvalue.py:67-143` returns the same map)."""
+        values = self.compute_eigenvalue(module, loss=loss, device=device, scale=scale)
+        out = {}
+        for i, (block, v) in enumerate(zip(self.get_layers(module), values)):
+            for p in block.parameters():
+                out[id(p)] = (v if v != 0.0 else 1.0, i)
+        return out

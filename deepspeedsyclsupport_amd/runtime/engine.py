@@ -122,6 +122,55 @@ class DeepSpeedEngine(nn.Module):
         if self._config.compression_config:
             from ..compression.compress import compression_scheduler
             self.compression_scheduler = compression_scheduler(self.module, self._config.compression_config)
+        self._configure_moq()
+        self.progressive_layer_drop = None
+        if self._config.pld_enabled:
+            from .progressive_layer_drop import ProgressiveLayerDrop
+            self.progressive_layer_drop = ProgressiveLayerDrop(theta=self._config.pld_params.get("theta", 1.0),
+                                                               gamma=self._config.pld_params.get("gamma", 0.001))
+
+    def _configure_moq(self):
+        """MoQ (reference `engine.py:1384-1401,1643-1655`): weight quantization with `quantize_weight_in_forward`
+        off quantises the 16-bit weights after every optimizer step on a per-weight bit schedule, optionally
+        stretched per block by Hessian eigenvalues."""
+        self.quantizer, self.eigenvalue, self.block_eigenvalue = None, None, None
+        self.gas_boundary_ctr = 0
+        c = self._config
+        if c.eigenvalue_enabled:
+            from .eigenvalue import Eigenvalue
+            self.eigenvalue = Eigenvalue(verbose=c.eigenvalue_verbose, max_iter=c.eigenvalue_max_iter,
+                                         tol=c.eigenvalue_tol, stability=c.eigenvalue_stability,
+                                         gas_boundary_resolution=c.eigenvalue_gas_boundary_resolution,
+                                         layer_name=c.eigenvalue_layer_name, layer_num=c.eigenvalue_layer_num)
+        wq = (c.compression_config or {}).get("weight_quantization", {}).get("shared_parameters", {})
+        if not wq.get("enabled", False) or wq.get("quantize_weight_in_forward", False):
+            return
+        from .quantize import Quantizer
+        self.quantizer = Quantizer(q_groups=wq.get("quantize_groups", 1),
+                                   q_mixed_fp16=wq.get("fp16_mixed_quantize", {}).get("enabled", False),
+                                   q_change_ratio=wq.get("fp16_mixed_quantize", {}).get("quantize_change_ratio",
+                                                                                        0.001),
+                                   q_type=wq.get("quantization_type", "symmetric"),
+                                   q_rounding=wq.get("rounding", "nearest"), q_verbose=wq.get("quantize_verbose",
+                                                                                              False),
+                                   q_eigenvalue=c.eigenvalue_enabled,
+                                   use_quantizer_kernel=wq.get("quantizer_kernel", False),
+                                   layer_num=c.eigenvalue_layer_num if c.eigenvalue_enabled else 0)
+        if self.compression_scheduler is not None:
+            self.compression_scheduler.moq_external = True
+
+    def _moq_quantize(self, block_eigenvalue=None):
+        if self.quantizer is None or self.compression_scheduler is None or \
+                not self.compression_scheduler.weight_quantization_enabled:
+            return
+        overflow = bool(self.optimizer.overflow) if (self.optimizer is not None and self.fp16_enabled()) else False
+        self.quantizer.quantize([list(self.module.parameters())], overflow, self.eigenvalue is not None,
+                                block_eigenvalue)
+
+    def _eigenvalue_due(self):
+        return (self.eigenvalue is not None and self.quantizer is not None and
+                (self.gas_boundary_ctr + 1) % self.eigenvalue.gas_boundary_resolution == 0 and
+                self.quantizer.any_precision_switch())
 
     def _configure_autotuning(self):
         """Autotuning experiment mode (reference engine.py autotuning hooks): report model info, or measure the
@@ -443,6 +492,13 @@ class DeepSpeedEngine(nn.Module):
             d = self.curriculum_scheduler_legacy.update_difficulty(self.global_steps + 1)
             if self._module_accepts("curriculum_seqlen"):
                 kwargs["curriculum_seqlen"] = d
+        if self.global_steps == 0 and self.micro_steps == 0 and self.compression_scheduler is not None and \
+                self.module.training:
+            # techniques with schedule_offset 0 switch on before the first forward (reference engine.py:1796-1807)
+            self.compression_scheduler.step(step_zero_check=0)
+            self._moq_quantize()
+        if self.module.training and self.progressive_layer_drop is not None:
+            kwargs.update(self.progressive_layer_drop.get_state())
         loss = self.module(*inputs, **kwargs)
         self.timers(FORWARD_MICRO_TIMER).stop()
         return loss
@@ -466,6 +522,12 @@ class DeepSpeedEngine(nn.Module):
             self.monitor.write_events([("Train/Samples/train_loss", float(loss.detach()) *
                                         self.gradient_accumulation_steps(), self.global_samples)])
         self.optimizer.is_gradient_accumulation_boundary = self.is_gradient_accumulation_boundary()
+        if self.is_gradient_accumulation_boundary() and self._eigenvalue_due():
+            # Hessian power iteration on this micro-batch's graph before the regular backward consumes it
+            log_dist("computing eigenvalue...", ranks=[0])
+            self.block_eigenvalue = self.eigenvalue.compute_block_eigenvalue(
+                self.module, loss=loss, device=self.device, scale=float(self.optimizer.cur_scale))
+            retain_graph = True
         self.optimizer.backward(loss, retain_graph=retain_graph)
         self.timers(BACKWARD_MICRO_TIMER).stop()
         return loss
@@ -480,6 +542,9 @@ class DeepSpeedEngine(nn.Module):
     def step(self, lr_kwargs=None):
         self.timers(STEP_MICRO_TIMER).start()
         if self.is_gradient_accumulation_boundary():
+            self.gas_boundary_ctr += 1
+            if self.progressive_layer_drop is not None:
+                self.progressive_layer_drop.update_state(self.global_steps)
             if self.optimizer is not None:
                 self.optimizer.step()
                 overflow = self.optimizer.overflow
@@ -489,6 +554,9 @@ class DeepSpeedEngine(nn.Module):
                     self.lr_scheduler.step(**(lr_kwargs or {}))
                 if self.optimizer.coordinator is not None:
                     self.optimizer.coordinator.reset_step()
+                use_ev = self.eigenvalue is not None and \
+                    self.gas_boundary_ctr % self.eigenvalue.gas_boundary_resolution == 0
+                self._moq_quantize(self.block_eigenvalue if use_ev else None)
             self.global_steps += 1
             self.global_samples += self.train_batch_size()
             if self.compression_scheduler is not None:
