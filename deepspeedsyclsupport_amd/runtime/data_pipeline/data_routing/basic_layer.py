@@ -58,6 +58,23 @@ def token_sort_(indices):
     return torch.sort(indices, dim=-1).values
 
 
+def mask_gather_gpt(mask, reserved_length):
+    """Causal mask of the kept tokens: they keep their relative order, so it is the leading k x k block (reference
+    `ops/random_ltd/dropping_utils.py:18-42` gpt_sample_tokens)."""
+    return mask[..., :reserved_length, :reserved_length]
+
+
+def mask_gather_bert(mask, idx):
+    """Encoder mask [B, 1, Sq, S] (or [B, 1, 1, S] key-padding) restricted to the kept positions idx [B, k] on both
+    the query and the key axis (reference `dropping_utils.py:52-79` bert_sample_tokens / `slice_attn_masks.cu`)."""
+    B, k = idx.shape
+    if mask.shape[-2] != 1:
+        rows = idx.view(B, 1, k, 1).expand(B, mask.shape[1], k, mask.shape[-1])
+        mask = torch.gather(mask, 2, rows)
+    cols = idx.view(B, 1, 1, k).expand(B, mask.shape[1], mask.shape[2], k)
+    return torch.gather(mask, 3, cols)
+
+
 def token_gather(x, idx, batch_first=True):
     """x [B, S, H] (or [S, B, H]) -> [B, k, H] keeping positions idx [B, k]."""
     if not batch_first:
@@ -86,11 +103,17 @@ class RandomLayerTokenDrop(nn.Module):
         self.random_ltd_scheduler = None
         self.random_ltd_num_layer = None
         self.random_ltd_initialized = False
+        self.mask_name = None
+        self.model_type = "decoder"
 
     def init_config(self, config, scheduler, random_ltd_layer_id):
         self.random_ltd_scheduler = scheduler
         self.random_ltd_layer_id = random_ltd_layer_id
         self.random_ltd_initialized = True
+        self.mask_name = config.get("model_mask_name")
+        self.model_type = config.get("model_type", "decoder")
+        if "hidden_state_order" in config:
+            self.batch_first = config["hidden_state_order"] == "batch_seq_dim"
 
     def forward(self, hidden_states, *args, **kwargs):
         if self.random_ltd_scheduler is not None:
@@ -101,6 +124,11 @@ class RandomLayerTokenDrop(nn.Module):
         B = hidden_states.shape[0 if self.batch_first else 1]
         keys = torch.rand(B, S, device=hidden_states.device)
         idx = token_sort_(torch.topk(keys, self.reserved_length, dim=-1).indices)
+        if self.mask_name is not None and kwargs.get(self.mask_name) is not None:
+            m = kwargs[self.mask_name]
+            kwargs = dict(kwargs)
+            kwargs[self.mask_name] = mask_gather_bert(m, idx) if self.model_type == "encoder" else \
+                mask_gather_gpt(m, self.reserved_length)
         native = self.batch_first and _native(hidden_states)
         if native:
             flat = _flat(idx, S)

@@ -66,3 +66,41 @@ def test_random_ltd_layer():
     layer.eval()
     sch.set_current_seq(4)
     torch.testing.assert_close(layer(x), lin(x))
+
+
+def test_random_ltd_mask_slicing():
+    """Encoder masks are gathered on both axes at the kept positions, decoder causal masks keep their k x k corner
+    (reference `ops/random_ltd/dropping_utils.py` bert/gpt_sample_tokens)."""
+    from deepspeedsyclsupport_amd.runtime.data_pipeline.data_routing.basic_layer import (RandomLayerTokenDrop,
+                                                                                          mask_gather_bert,
+                                                                                          mask_gather_gpt)
+    B, S, k = 2, 6, 3
+    full = torch.arange(B * S * S, dtype=torch.float32).view(B, 1, S, S)
+    idx = torch.tensor([[0, 2, 5], [1, 3, 4]])
+    got = mask_gather_bert(full, idx)
+    for b in range(B):
+        torch.testing.assert_close(got[b, 0], full[b, 0][idx[b]][:, idx[b]])
+    pad = torch.arange(B * S, dtype=torch.float32).view(B, 1, 1, S)
+    torch.testing.assert_close(mask_gather_bert(pad, idx)[:, 0, 0], torch.gather(pad[:, 0, 0], 1, idx))
+    causal = torch.tril(torch.ones(S, S)).view(1, 1, S, S)
+    torch.testing.assert_close(mask_gather_gpt(causal, k), torch.tril(torch.ones(k, k)).view(1, 1, k, k))
+
+    class Layer(torch.nn.Module):
+
+        def forward(self, x, attention_mask=None):
+            self.seen = attention_mask.shape
+            return x * 2
+
+    class Sched:
+
+        def get_current_seq(self):
+            return k
+
+    lyr = RandomLayerTokenDrop(Layer())
+    lyr.init_config({"model_mask_name": "attention_mask", "model_type": "encoder"}, Sched(), 0)
+    lyr.train()
+    x = torch.randn(B, S, 4)
+    out = lyr(x, attention_mask=full)
+    assert lyr.random_ltd_layer.seen == (B, 1, k, k)
+    changed = (out != x).any(-1).sum(1)
+    assert changed.tolist() == [k, k]
