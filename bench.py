@@ -150,7 +150,10 @@ def main():
             "reduce_bucket_size": int(2e8),
             "stage3_prefetch_bucket_size": int(2e8),
             "stage3_param_persistence_threshold": int(1e5),
-            "stage3_max_live_parameters": int(3e9),
+            # sized for 288 GB of HBM: the whole bf16 model (13.4 GB at 7B) may stay gathered from a layer's forward
+            # to its backward, so each partitioned parameter is all-gathered once per step, not twice
+            "stage3_max_live_parameters": int(1e10),
+            "stage3_max_reuse_distance": int(1e10),
         },
     }
     assert world % args.sp == 0, "--sp must divide the number of ranks"

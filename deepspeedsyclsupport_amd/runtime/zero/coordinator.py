@@ -9,6 +9,12 @@ Per fetch group (one module's params in one flat buffer):
 The trace of group fetches is recorded on the first step and replayed: at trace position i the coordinator issues
 `all_gather_into_tensor` on the dedicated `ag_stream` for the next groups up to `prefetch_bucket_size` elements,
 so xGMI transfers run under the current layer's GEMMs. A divergent fetch order invalidates the trace (re-record).
+
+Reuse distance (reference `stage3_max_reuse_distance`, `partitioned_param_coordinator.py:389-416`): after a
+module's forward, a group whose next fetch in the trace comes within `max_reuse_distance` gathered elements stays
+gathered (within `max_live_parameters`). Sized for 288 GB of HBM — a 7B model's full bf16 weights are 13.4 GB — the
+last layers' (or, with a large budget, every layer's) forward gather is reused by the backward instead of being
+re-gathered over xGMI: one all-gather per parameter per step instead of two.
 """
 import torch
 
@@ -23,10 +29,13 @@ RECORD, COMPLETE, INVALID = 0, 1, 2
 
 class ParamCoordinator:
 
-    def __init__(self, opt, prefetch_bucket_size=int(5e7), max_live_parameters=int(1e9)):
+    def __init__(self, opt, prefetch_bucket_size=int(5e7), max_live_parameters=int(1e9),
+                 max_reuse_distance=int(1e9)):
         self.opt = opt
         self.prefetch_bucket_size = int(prefetch_bucket_size)
         self.max_live = int(max_live_parameters)
+        self.max_reuse = int(max_reuse_distance)
+        self._reuse_dist = []  # per trace position: gathered elements until the same group's next fetch (or None)
         self.trace = []
         self.mode = RECORD
         self.pos = 0
@@ -104,7 +113,20 @@ class ParamCoordinator:
     def _post_fwd(self, m, inputs, outputs):
         if self.in_backward or torch._C._current_graph_task_id() != -1:
             return  # activation-checkpoint recompute inside backward: keep params for the module's backward
-        self.release(m._ds_fetch_group)
+        g = m._ds_fetch_group
+        if self._keep_for_reuse(g):
+            return
+        self.release(g)
+
+    def _keep_for_reuse(self, g):
+        """Keep a just-used group gathered when the trace says it is fetched again soon enough."""
+        if self.mode != COMPLETE or self.max_reuse <= 0 or g.persistent:
+            return False
+        p = getattr(g, "_ds_trace_pos", None)
+        if p is None or p >= len(self._reuse_dist):
+            return False
+        d = self._reuse_dist[p]
+        return d is not None and d <= self.max_reuse and self.live_numel <= self.max_live
 
     def _pre_bwd(self, m, grad_output):
         self.fetch(m._ds_fetch_group)
@@ -197,6 +219,7 @@ class ParamCoordinator:
             return
         if self.mode == COMPLETE:
             if self.pos < len(self.trace) and self.trace[self.pos] == g.idx:
+                g._ds_trace_pos = self.pos
                 self.pos += 1
             else:
                 logger.debug("ZeRO-3 fetch order diverged from the recorded trace; re-recording")
@@ -217,6 +240,20 @@ class ParamCoordinator:
             budget -= g.numel
             i += 1
 
+    def _reuse_distances(self):
+        """For each trace position, the elements gathered between it and the next fetch of the same group."""
+        groups = self.opt.groups
+        prefix = [0]
+        for gi in self.trace:
+            prefix.append(prefix[-1] + groups[gi].numel)
+        nxt, out = {}, [None] * len(self.trace)
+        for p in range(len(self.trace) - 1, -1, -1):
+            gi = self.trace[p]
+            if gi in nxt:
+                out[p] = prefix[nxt[gi]] - prefix[p + 1]
+            nxt[gi] = p
+        return out
+
     def begin_backward(self):
         self.in_backward = True
 
@@ -231,6 +268,7 @@ class ParamCoordinator:
                 assert_ints_same_as_other_ranks(trace_digest(self.trace), self.opt.dp_group,
                                                 "recorded ZeRO-3 fetch trace (length, digest)")
             self.mode = COMPLETE if self.trace else RECORD
+            self._reuse_dist = self._reuse_distances()
         elif self.mode == INVALID:
             self.trace = []
             self.mode = RECORD

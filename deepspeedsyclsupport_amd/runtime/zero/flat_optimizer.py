@@ -198,7 +198,8 @@ class FlatZeroOptimizer:
         if self.stage == 3 and (self.dp > 1 or self.offload_param or self.force_partition):
             from .coordinator import ParamCoordinator
             self.coordinator = ParamCoordinator(self, prefetch_bucket_size=self.zc.prefetch_bucket_size,
-                                                max_live_parameters=self.zc.max_live_parameters)
+                                                max_live_parameters=self.zc.max_live_parameters,
+                                                max_reuse_distance=self.zc.max_reuse_distance)
         log_dist(f"FlatZeroOptimizer: stage={self.stage} dp={self.dp} groups={len(self.groups)} "
                  f"params={sum(g.numel for g in self.groups) / 1e6:.1f}M partition={self.partition} "
                  f"offload={self.offload}(ratio={self.offload_ratio}) offload_param={self.offload_param} "

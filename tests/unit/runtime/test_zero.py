@@ -158,3 +158,50 @@ def test_on_device_meta():
     with OnDevice(dtype=torch.bfloat16, device="meta"):
         m = torch.nn.Linear(1000, 1000)
     assert m.weight.device.type == "meta" and m.weight.dtype == torch.bfloat16
+
+
+def _reuse_run(reuse, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    rank = dist.get_rank()
+    model = tiny_llama()
+    cfg = base_config(stage=3, lr=1e-3, mb=2, gas=1, clip=1.0)
+    cfg["zero_optimization"].update({"stage3_param_persistence_threshold": 0, "stage3_max_reuse_distance": reuse,
+                                     "stage3_max_live_parameters": int(1e9)})
+    eng, _, _, _ = ds.initialize(model=model, config=cfg)
+    coord = eng.optimizer.coordinator
+    gathers = [0]
+    orig = coord._gather
+
+    def counted(g):
+        gathers[0] += 1
+        return orig(g)
+
+    coord._gather = counted
+    data = random_tokens(4, 2, 16, seed=100 + rank)
+    losses, per_step = [], []
+    for s in range(4):
+        before = gathers[0]
+        loss = eng(data[s], labels=data[s])
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss))
+        per_step.append(gathers[0] - before)
+    if rank == 0:
+        torch.save({"losses": losses, "gathers": per_step, "n_groups": sum(not g.persistent
+                                                                            for g in eng.optimizer.groups)}, out)
+
+
+def test_zero3_reuse_distance_skips_backward_gathers(tmp_path):
+    """stage3_max_reuse_distance: with a budget covering the whole step each group is gathered once per step
+    (forward) and reused by its backward; with 0 it is gathered again for backward. Same numerics."""
+    res = {}
+    for reuse in (0, int(1e10)):
+        out = str(tmp_path / f"r{reuse}.pt")
+        run_distributed(_reuse_run, 2, reuse, out)
+        res[reuse] = torch.load(out, weights_only=True)
+    n = res[0]["n_groups"]
+    # step 1 records the trace (no reuse yet); afterwards: 2 gathers per group without reuse, 1 with
+    assert res[0]["gathers"][1:] == [2 * n] * 3
+    assert res[int(1e10)]["gathers"][1:] == [n] * 3
+    assert res[0]["losses"] == res[int(1e10)]["losses"]
