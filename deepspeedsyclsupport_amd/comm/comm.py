@@ -128,6 +128,11 @@ def init_distributed(dist_backend=None, auto_mpi_discovery=True, distributed_por
         dist_backend = get_accelerator().communication_backend_name()
     required = ["RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"]
     if not all(k in os.environ for k in required):
+        if in_aml() and not in_dlts():
+            patch_aml_env_for_torch_nccl_backend(master_port=distributed_port, verbose=verbose)
+        elif in_aws_sm():
+            patch_aws_sm_env_for_torch_nccl_backend(verbose=verbose)
+    if not all(k in os.environ for k in required):
         if auto_mpi_discovery and _mpi_env_discovery(distributed_port, verbose):
             pass
         elif rank < 0:
@@ -169,6 +174,69 @@ def _mpi_env_discovery(port, verbose):
                 logger.info(f"Discovered MPI-style env via {r}: rank={os.environ['RANK']} world={os.environ['WORLD_SIZE']}")
             return True
     return False
+
+
+def mpi_discovery(distributed_port=TORCH_DISTRIBUTED_DEFAULT_PORT, verbose=True):
+    """Reference name (`comm.py:673`): the launcher env of OpenMPI / MPICH / Slurm mapped to the torch env vars
+    (mpi4py is not part of this stack; the MPI launchers export everything needed)."""
+    if not _mpi_env_discovery(distributed_port, verbose):
+        raise RuntimeError("mpi_discovery: no OpenMPI / MPICH / Slurm rank variables in the environment")
+    if is_initialized():
+        assert get_rank() == int(os.environ["RANK"]) and get_world_size() == int(os.environ["WORLD_SIZE"]), \
+            "MPI rank / world size disagree with the initialised process group"
+
+
+def in_aml():
+    """Azure Machine Learning job (reference `comm.py:714`)."""
+    return "AZUREML_EXPERIMENT_ID" in os.environ
+
+
+def in_aws_sm():
+    """AWS SageMaker job."""
+    return "SM_TRAINING_ENV" in os.environ
+
+
+def in_dlts():
+    return "DLTS_JOB_ID" in os.environ
+
+
+def patch_aml_env_for_torch_nccl_backend(master_port=6105, verbose=True):
+    """AzureML exports OpenMPI ranks and its own master-node variables (reference `comm.py:729-760`)."""
+    os.environ["RANK"] = os.environ["OMPI_COMM_WORLD_RANK"]
+    os.environ["WORLD_SIZE"] = os.environ["OMPI_COMM_WORLD_SIZE"]
+    os.environ["LOCAL_RANK"] = os.environ["OMPI_COMM_WORLD_LOCAL_RANK"]
+    single_node = int(os.environ.get("OMPI_COMM_WORLD_LOCAL_SIZE", os.environ["WORLD_SIZE"])) == \
+        int(os.environ["WORLD_SIZE"])
+    if single_node:
+        os.environ["MASTER_ADDR"] = os.environ.get("AZ_BATCHAI_MPI_MASTER_NODE", "127.0.0.1")
+        os.environ["MASTER_PORT"] = os.environ.get("MASTER_PORT", "54965")
+    else:
+        os.environ["MASTER_ADDR"] = os.environ["AZ_BATCH_MASTER_NODE"].split(":")[0]
+        os.environ.setdefault("MASTER_PORT", str(master_port))
+    os.environ["NCCL_SOCKET_IFNAME"] = os.environ.get("NCCL_SOCKET_IFNAME", "^docker0,lo")
+    if verbose:
+        logger.info(f"AzureML env: rank={os.environ['RANK']} local_rank={os.environ['LOCAL_RANK']} "
+                    f"world={os.environ['WORLD_SIZE']} master={os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}")
+
+
+def patch_aws_sm_env_for_torch_nccl_backend(verbose=True):
+    """SageMaker exports OpenMPI ranks; MASTER_ADDR / MASTER_PORT come from the job (reference `comm.py:763-771`)."""
+    os.environ["RANK"] = os.environ["OMPI_COMM_WORLD_RANK"]
+    os.environ["LOCAL_RANK"] = os.environ["OMPI_COMM_WORLD_LOCAL_RANK"]
+    os.environ["WORLD_SIZE"] = os.environ["OMPI_COMM_WORLD_SIZE"]
+    if verbose:
+        logger.info(f"SageMaker env: rank={os.environ['RANK']} world={os.environ['WORLD_SIZE']}")
+
+
+def set_backend():
+    """API parity (reference `comm.py:198`): there is one backend here, torch.distributed over RCCL / gloo."""
+    return None
+
+
+def init_deepspeed_backend(ds_backend=None, timeout=default_pg_timeout, init_method=None):
+    """API parity (reference `comm.py:143`, whose only native backend is oneCCL): nothing beyond torch.distributed
+    is initialised here; the xGMI inference all-reduce sets itself up lazily (comm/xgmi.py)."""
+    return None
 
 
 def destroy_process_group(group=None):
@@ -247,6 +315,18 @@ def inference_all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, **
 
 
 @timed_op
+def has_all_reduce_coalesced():
+    return hasattr(tdist, "all_reduce_coalesced")
+
+
+def all_gather_coalesced(output_tensors, input_tensors, group=None, async_op=False):
+    """Per-tensor all-gathers issued as one coalesced batch (reference `comm.py:250`)."""
+    with tdist._coalescing_manager(group=group, async_ops=async_op) as cm:
+        for out, inp in zip(output_tensors, input_tensors):
+            tdist.all_gather_into_tensor(out, inp, group=group)
+    return cm if async_op else None
+
+
 def all_reduce_coalesced(tensors, op=ReduceOp.SUM, group=None, async_op=False, **kw):
     return tdist.all_reduce_coalesced(tensors, op=op, group=group, async_op=async_op)
 
