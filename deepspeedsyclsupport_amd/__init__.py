@@ -23,6 +23,40 @@ from .runtime.lr_schedules import add_tuning_arguments  # noqa: E402,F401
 from .utils.logging import log_dist, logger  # noqa: E402,F401
 
 
+# the rest of the reference's top-level names, imported on first use (keeps `import` light and cycle-free)
+_LAZY = {
+    "ops": (".ops", None),
+    "module_inject": (".module_inject", None),
+    "DeepSpeedHybridEngine": (".runtime.hybrid_engine", "DeepSpeedHybridEngine"),
+    "PipelineEngine": (".runtime.pipe.engine", "PipelineEngine"),
+    "PipelineModule": (".runtime.pipe.module", "PipelineModule"),
+    "InferenceEngine": (".inference.engine", "InferenceEngine"),
+    "DeepSpeedInferenceConfig": (".inference.config", "DeepSpeedInferenceConfig"),
+    "checkpointing": (".runtime.activation_checkpointing", "checkpointing"),
+    "DeepSpeedTransformerLayer": (".ops.transformer", "DeepSpeedTransformerLayer"),
+    "DeepSpeedTransformerConfig": (".ops.transformer", "DeepSpeedTransformerConfig"),
+    "replace_transformer_layer": (".module_inject.replace_module", "replace_transformer_layer"),
+    "revert_transformer_layer": (".module_inject.replace_module", "revert_transformer_layer"),
+    "OnDevice": (".utils.init_on_device", "OnDevice"),
+    "DeepSpeedOptimizer": (".runtime", "DeepSpeedOptimizer"),
+    "ZeROOptimizer": (".runtime", "ZeROOptimizer"),
+    "ADAM_OPTIMIZER": (".runtime.config", "ADAM_OPTIMIZER"),
+    "LAMB_OPTIMIZER": (".runtime.config", "LAMB_OPTIMIZER"),
+}
+git_hash, git_branch = __git_hash__, __git_branch__
+
+
+def __getattr__(name):
+    if name not in _LAZY:
+        raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+    import importlib
+    mod, attr = _LAZY[name]
+    m = importlib.import_module(mod, __name__)
+    val = m if attr is None else getattr(m, attr)
+    globals()[name] = val
+    return val
+
+
 def _parse_version(s):
     return tuple(int(x) for x in s.split(".")[:3])
 
@@ -40,6 +74,8 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
     if config is None and args is not None:
         config = getattr(args, "deepspeed_config", None)
     assert config is not None, "DeepSpeed requires --deepspeed_config or config=..."
+    if args is not None and getattr(args, "deepspeed_mpi", False):
+        comm.mpi_discovery()
     if dist_init_required is not False:
         init_distributed(dist_init_required=dist_init_required)
     try:

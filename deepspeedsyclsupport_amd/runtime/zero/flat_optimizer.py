@@ -38,6 +38,7 @@ from ...checkpoint import constants as CK
 from ...ops import native
 from ...ops.adam.fused_adam import FusedAdam
 from ...utils.logging import log_dist, logger
+from .. import ZeROOptimizer
 from ..fp16.loss_scaler import CreateLossScaler
 from .config import ZeroStageEnum
 from ...utils.nvtx import instrument_w_nvtx
@@ -112,7 +113,7 @@ class FlatGroup:
         return out
 
 
-class FlatZeroOptimizer:
+class FlatZeroOptimizer(ZeROOptimizer):
     """ZeRO stage 0/1/2/3 over flat groups. See module docstring."""
 
     def __init__(self, init_optimizer, module, ds_config, dp_group=None, stage=0, mpu=None, clip_grad=0.0,

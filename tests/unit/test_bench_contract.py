@@ -36,3 +36,16 @@ def test_bench_two_rank_dryrun_prints_one_json_line(extra):
     assert rec["value"] > 0 and rec["higher_is_better"] is True
     assert rec["config"]["parallelism"] == ("dp1-sp2" if extra else "dp2")
     assert rec["final_loss"] == rec["final_loss"]  # not NaN
+
+
+def test_top_level_api_names():
+    """Every public top-level name of the reference's `deepspeed/__init__.py` resolves here."""
+    import deepspeedsyclsupport_amd as ds
+    for name in ("initialize", "init_inference", "init_distributed", "add_config_arguments", "default_inference_config",
+                 "DeepSpeedEngine", "DeepSpeedHybridEngine", "PipelineEngine", "PipelineModule", "InferenceEngine",
+                 "DeepSpeedInferenceConfig", "DeepSpeedConfig", "DeepSpeedConfigError", "checkpointing",
+                 "DeepSpeedTransformerLayer", "DeepSpeedTransformerConfig", "replace_transformer_layer",
+                 "revert_transformer_layer", "OnDevice", "zero", "DeepSpeedOptimizer", "ZeROOptimizer",
+                 "ADAM_OPTIMIZER", "LAMB_OPTIMIZER", "log_dist", "logger", "get_accelerator", "add_tuning_arguments",
+                 "ops", "module_inject", "comm", "version", "git_hash", "git_branch"):
+        assert getattr(ds, name) is not None or name in ("git_hash", "git_branch"), name
