@@ -104,3 +104,35 @@ def test_random_ltd_mask_slicing():
     assert lyr.random_ltd_layer.seen == (B, 1, k, k)
     changed = (out != x).any(-1).sum(1)
     assert changed.tolist() == [k, k]
+
+
+def test_random_ltd_ops_frontend():
+    """ops/random_ltd: sampled indices are sorted and distinct; GatherTokens / ScatterTokens are exact adjoints."""
+    from deepspeedsyclsupport_amd.ops.random_ltd import GatherTokens, ScatterTokens, gpt_sample_tokens
+    idx, mask = gpt_sample_tokens(4, 10, 3, layers=2, attn_mask=torch.tril(torch.ones(1, 1, 10, 10)))
+    assert idx.shape == (2, 3, 4) and idx.dtype == torch.int32 and mask.shape == (1, 1, 4, 4)
+    assert (idx[..., 1:] > idx[..., :-1]).all()
+    x = torch.randn(3, 10, 8, requires_grad=True)
+    acts, part = GatherTokens.apply(x, idx[0], True)
+    torch.testing.assert_close(part, torch.stack([x[b, idx[0, b].long()] for b in range(3)]))
+    full = ScatterTokens.apply(acts, part * 2, idx[0], True)
+    full.sum().backward()
+    # kept tokens were doubled and scattered back over themselves: d/dx = 2 on the kept set, 1 (bypass) elsewhere
+    g = x.grad
+    for b in range(3):
+        keep = set(idx[0, b].tolist())
+        for s in range(10):
+            assert torch.allclose(g[b, s], torch.full((8, ), 2.0 if s in keep else 1.0))
+
+
+def test_utils_reference_paths():
+    from deepspeedsyclsupport_amd.utils import debug, numa
+    from deepspeedsyclsupport_amd.utils.groups import _get_data_parallel_world_size  # noqa: F401
+    from deepspeedsyclsupport_amd.utils.types import GATED_ACTIVATION_TYPES, ActivationFuncType
+    assert ActivationFuncType.GATED_SILU in GATED_ACTIVATION_TYPES
+    assert numa.parse_range_list("0-2,5,7-8") == [0, 1, 2, 5, 7, 8]
+    per, cmd = numa.get_numactl_cmd("0-7", 4, 2)
+    assert per == 2 and cmd[0] == "numactl" and cmd[-1] == "4,5"
+    m = torch.nn.Linear(2, 2)
+    debug.debug_extract_module_and_param_names(m)
+    assert debug.debug_param2name(m.weight) == "weight"
