@@ -16,6 +16,7 @@ int ds_grouped_gemm(const void*, const void*, void*, const int*, int, int, int, 
 int ds_embed_gather(const void*, const int64_t*, const void*, const int64_t*, void*, int64_t, int, hipStream_t);
 int ds_rows_gather(const void*, const int64_t*, void*, int64_t, int, hipStream_t);
 int ds_rows_scatter(const void*, const int64_t*, void*, int64_t, int, hipStream_t);
+int ds_token_sort(int*, int, int, int, hipStream_t);
 }
 
 using torch::Tensor;
@@ -116,6 +117,16 @@ Tensor embed_gather(Tensor table, Tensor ids, std::optional<Tensor> pos_table, s
 }
 
 // out[i] = x[idx[i]] rows
+// In-place per-row sort of distinct int32 token positions in [0, S) (random-LTD token_sort_).
+Tensor token_sort_(Tensor idx, int64_t S) {
+  need(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.dim() >= 1, "token_sort_: int32 indices");
+  const int64_t k = idx.size(-1);
+  TORCH_CHECK(k <= S && S <= (1 << 20), "token_sort_: need k <= S <= 2^20");
+  check(ds_token_sort(idx.data_ptr<int>(), (int)(idx.numel() / k), (int)k, (int)S, stream()), "token_sort_");
+  return idx;
+}
+
 Tensor rows_gather(Tensor x, Tensor idx) {
   need_bf16(x, "x"); need(idx, "idx");
   TORCH_CHECK(idx.scalar_type() == at::kLong, "idx must be int64");
@@ -143,6 +154,7 @@ void register_moe_ops(pybind11::module& m) {
   m.def("grouped_gemm_ok", &grouped_gemm_ok);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("embed_gather", &embed_gather);
+  m.def("token_sort_", &token_sort_);
   m.def("rows_gather", &rows_gather);
   m.def("rows_scatter", &rows_scatter);
 }

@@ -360,3 +360,63 @@ extern "C" int ds_rows_scatter(const void* part, const int64_t* idx, void* full,
   DS_CHECK_LAUNCH();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------ random-LTD token sort
+// Sort each row of k DISTINCT token positions in [0, S) (reference `csrc/random_ltd/token_sort.cu:28` scan_sort):
+// because the values are distinct and bounded, the sorted row is the compaction of a bitmap. One workgroup per row:
+// set the row's bits in an LDS bitmap (S/32 words), popcount each thread's contiguous word range, one exclusive scan
+// over the 256 per-thread counts, then every thread writes its positions in order. O(S + k) per row, no comparisons.
+namespace {
+constexpr int TS_THREADS = 256;
+__global__ void __launch_bounds__(TS_THREADS) token_sort_kernel(int* __restrict__ idx, int k, int S) {
+  extern __shared__ unsigned int bm[];  // [words] bitmap, then [TS_THREADS] scan scratch
+  const int words = (S + 31) >> 5;
+  unsigned int* scan = bm + words;
+  int* row = idx + (int64_t)blockIdx.x * k;
+  for (int w = threadIdx.x; w < words; w += TS_THREADS) bm[w] = 0u;
+  __syncthreads();
+  for (int i = threadIdx.x; i < k; i += TS_THREADS) {
+    const int v = row[i];
+    if (v >= 0 && v < S) atomicOr(&bm[v >> 5], 1u << (v & 31));
+  }
+  __syncthreads();
+  const int per = (words + TS_THREADS - 1) / TS_THREADS;
+  const int w0 = min(threadIdx.x * per, words), w1 = min(w0 + per, words);
+  unsigned int cnt = 0;
+  for (int w = w0; w < w1; ++w) cnt += __popc(bm[w]);
+  scan[threadIdx.x] = cnt;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 256 counts (8 steps)
+  for (int off = 1; off < TS_THREADS; off <<= 1) {
+    const unsigned int add = threadIdx.x >= off ? scan[threadIdx.x - off] : 0u;
+    __syncthreads();
+    scan[threadIdx.x] += add;
+    __syncthreads();
+  }
+  int pos = (int)(scan[threadIdx.x] - cnt);
+  for (int w = w0; w < w1; ++w) {
+    unsigned int bits = bm[w];
+    while (bits) {
+      const int b = __ffs(bits) - 1;
+      bits &= bits - 1;
+      if (pos < k) row[pos] = (w << 5) + b;
+      ++pos;
+    }
+  }
+}
+}  // namespace
+
+// idx [rows, k] int32 distinct values in [0, S), sorted in place per row.
+extern "C" int ds_token_sort(int* idx, int rows, int k, int S, hipStream_t s) {
+  if (rows <= 0 || k <= 0) return 0;
+  if (S <= 0 || k > S || S > (1 << 20)) return (int)hipErrorInvalidValue;
+  const size_t lds = ((size_t)(S + 31) / 32 + TS_THREADS) * sizeof(unsigned int);
+  static bool big = false;
+  if (lds > 65536 && !big) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&token_sort_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    big = true;
+  }
+  hipLaunchKernelGGL(token_sort_kernel, dim3(rows), dim3(TS_THREADS), lds, s, idx, k, S);
+  return (int)hipGetLastError();
+}

@@ -7,14 +7,15 @@ convention: GatherTokens returns (activations, gathered), ScatterTokens returns 
 import torch
 
 from ...runtime.data_pipeline.data_routing.basic_layer import (_flat, _native, mask_gather_bert, mask_gather_gpt,
-                                                                token_gather, token_scatter_)
+                                                                token_gather, token_scatter_, token_sort_)
 from .. import moe_ops
 
 
 def _sample(reserved_length, seq_length, batch_size, layers, device):
     keys = torch.rand(layers * batch_size, seq_length, device=device)
-    idx = torch.topk(keys, reserved_length, dim=-1).indices.sort(dim=-1).values
-    return idx.reshape(layers, batch_size, reserved_length).to(torch.int32)
+    idx = torch.topk(keys, reserved_length, dim=-1).indices.to(torch.int32)
+    idx = token_sort_(idx.contiguous(), seq_length)
+    return idx.reshape(layers, batch_size, reserved_length)
 
 
 def gpt_sample_tokens(reserved_length, seq_length, batch_size, layers=1, device="cpu", attn_mask=None):

@@ -54,7 +54,12 @@ class _TokenScatterFn(torch.autograd.Function):
         return gfull, gpart, None
 
 
-def token_sort_(indices):
+def token_sort_(indices, seq_length=None):
+    """Sort each row of distinct token positions. Device int32 rows go through the gfx950 bitmap-compaction kernel
+    (`moe_kernels.hip` token_sort_kernel, reference `csrc/random_ltd/token_sort.cu`), in place."""
+    if indices.is_cuda and seq_length is not None and indices.dtype == torch.int32 and indices.is_contiguous():
+        from ....ops.native import hip_ops
+        return hip_ops().token_sort_(indices, int(seq_length))
     return torch.sort(indices, dim=-1).values
 
 
@@ -123,7 +128,8 @@ class RandomLayerTokenDrop(nn.Module):
             return self.random_ltd_layer(hidden_states, *args, **kwargs)
         B = hidden_states.shape[0 if self.batch_first else 1]
         keys = torch.rand(B, S, device=hidden_states.device)
-        idx = token_sort_(torch.topk(keys, self.reserved_length, dim=-1).indices)
+        idx = torch.topk(keys, self.reserved_length, dim=-1).indices
+        idx = token_sort_(idx.to(torch.int32), S).long() if idx.is_cuda else token_sort_(idx)
         if self.mask_name is not None and kwargs.get(self.mask_name) is not None:
             m = kwargs[self.mask_name]
             kwargs = dict(kwargs)

@@ -123,3 +123,15 @@ def test_random_ltd_native_matches_index_ops():
     (out_r.float() ** 2).sum().backward()
     assert torch.equal(out, out_r)
     torch.testing.assert_close(g_native, x.grad, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("rows,S,k", [(16, 4096, 2048), (3, 100, 100), (8, 70000, 333), (2, 600000, 5000)])
+def test_token_sort_kernel(rows, S, k):
+    """Bitmap-compaction token sort (random-LTD token_sort_) == torch.sort on distinct positions, in place."""
+    from deepspeedsyclsupport_amd.ops.native import hip_ops
+    keys = torch.rand(rows, S, device="cuda")
+    idx = torch.topk(keys, k, dim=-1).indices.to(torch.int32).contiguous()
+    ref = torch.sort(idx, dim=-1).values
+    out = hip_ops().token_sort_(idx, S)
+    assert out.data_ptr() == idx.data_ptr()
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
