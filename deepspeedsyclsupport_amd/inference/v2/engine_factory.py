@@ -40,3 +40,45 @@ def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = 
     if q in ("int8", "int4"):
         ds_model.quantize_weights(8 if q == "int8" else 4)
     return InferenceEngineV2(ds_model, engine_config)
+
+
+def build_engine_from_ds_checkpoint(path, engine_config: RaggedInferenceEngineConfig = None, debug_level=0,
+                                    device=None):
+    """Rebuild an engine from `InferenceEngineV2.serialize(path)` output (reference `engine_factory.py:28`): the
+    model spec JSON plus this rank's safetensors shard — no HF checkpoint or transformers model needed. The job's
+    tensor-parallel degree must match the one the shards were written at."""
+    import json
+    import os
+
+    from safetensors.torch import load_file
+
+    from ..model_implementations.transformer import DSInferenceModel, DSModelSpec
+    engine_config = engine_config or RaggedInferenceEngineConfig()
+    with open(os.path.join(path, "ds_model_config.json")) as f:
+        fields = json.load(f)
+    fields["layer_windows"] = tuple(fields.get("layer_windows", ()))
+    spec = DSModelSpec(**fields)
+    meta_path = os.path.join(path, "ds_model_meta.json")
+    meta = json.load(open(meta_path)) if os.path.exists(meta_path) else {"dtype": "bfloat16", "tp_size": 1}
+    tp = engine_config.tensor_parallel.tp_size
+    if tp != meta["tp_size"]:
+        raise ValueError(f"checkpoint was serialized at tp={meta['tp_size']}, engine asks for tp={tp}")
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else \
+            torch.device("cpu")
+    group, rank = None, 0
+    if tp > 1:
+        from ... import comm as dist
+        world, me = dist.get_world_size(), dist.get_rank()
+        for s in range(0, world, tp):
+            g = dist.new_group(list(range(s, s + tp)))
+            if s <= me < s + tp:
+                group = g
+        rank = dist.get_rank(group)
+    model = DSInferenceModel(spec, group, tp, rank, to_dtype(meta["dtype"]), device)
+    sd = load_file(os.path.join(path, f"params_rank_{rank}.safetensors"), device=str(device))
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    if unexpected or any(not k.startswith(("rope_", "alibi")) for k in missing):
+        raise ValueError(f"serialized weights do not match the spec: missing {missing[:4]}, unexpected "
+                         f"{unexpected[:4]}")
+    return InferenceEngineV2(model, engine_config)

@@ -142,5 +142,8 @@ class InferenceEngineV2:
         from safetensors.torch import save_file
         sd = {k: v.detach().contiguous().cpu() for k, v in self._model.state_dict().items()}
         save_file(sd, os.path.join(save_path, f"params_rank_{self._model.tp_rank}.safetensors"))
-        with open(os.path.join(save_path, "ds_model_config.json"), "w") as f:
-            json.dump(dataclasses.asdict(self._model.spec), f)
+        if self._model.tp_rank == 0:
+            with open(os.path.join(save_path, "ds_model_config.json"), "w") as f:
+                json.dump(dataclasses.asdict(self._model.spec), f)
+            with open(os.path.join(save_path, "ds_model_meta.json"), "w") as f:
+                json.dump({"dtype": str(self._model.dtype).replace("torch.", ""), "tp_size": self._model.tp_size}, f)

@@ -108,3 +108,16 @@ def test_ragged_bf16_gpu(H):
     for u, p in prompts.items():
         ref = _ref(m, p, 5)
         assert outs[u][0] == ref[0] and sum(a == b for a, b in zip(outs[u], ref)) >= 3
+
+
+def test_serialize_and_rebuild_from_ds_checkpoint(tmp_path):
+    """serialize() + build_engine_from_ds_checkpoint() (reference engine_factory.py:28) rebuild an engine that
+    generates exactly what the original one did, without the HF model."""
+    from deepspeedsyclsupport_amd.inference.v2 import build_engine_from_ds_checkpoint
+    m = _model()
+    eng = _engine(m)
+    prompts = {0: torch.randint(0, 128, (7, )), 1: torch.randint(0, 128, (5, ))}
+    ref = _drive(eng, prompts, 4)
+    eng.serialize(str(tmp_path))
+    eng2 = build_engine_from_ds_checkpoint(str(tmp_path), eng._config, device=torch.device("cpu"))
+    assert _drive(eng2, prompts, 4) == ref
