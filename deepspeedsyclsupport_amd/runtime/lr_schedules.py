@@ -60,7 +60,6 @@ class LRRangeTest(_Sched):
         self.step_rate = lr_range_test_step_rate
         self.staircase = lr_range_test_staircase
         if last_batch_iteration == -1:
-            self.step(0) if False else None
             for pg, lr in zip(self.optimizer.param_groups, self.min_lr):
                 pg["lr"] = lr
             self._last_lr = list(self.min_lr)
@@ -117,6 +116,10 @@ class OneCycle(_Sched):
             return lrs
         decay_it = it - self.total
         interval = decay_it / self.decay_step_size if self.decay_step_size else 0
+        if self.cycle_momentum:  # after the cycle momentum returns to (and decays from) its max
+            for pg, hi in zip(self.optimizer.param_groups, self.max_moms):
+                if "betas" in pg:
+                    pg["betas"] = (hi[0] * (1 + self.decay_mom_rate * interval), pg["betas"][1])
         return [lo / (1 + self.decay_lr_rate * interval) for lo in self.min_lrs]
 
 
