@@ -101,7 +101,7 @@ class DeepSpeedEngine(nn.Module):
         self._configure_checkpointing()
         self._configure_data_efficiency()
         self._configure_autotuning()
-        if self._config.print_user_config if hasattr(self._config, "print_user_config") and False else False:
+        if self.global_rank == 0 and self._config.param_dict.get("print_config", False):
             self._config.print("DeepSpeedEngine configuration")
 
     # ============================================================================================ data efficiency
