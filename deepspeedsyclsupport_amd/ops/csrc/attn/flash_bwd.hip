@@ -31,7 +31,9 @@
 //    reuse in L2);
 //  * block-sparse: each workgroup walks only the 32-row query tiles its key block meets in the layout (a host-built
 //    column LUT) and masks at the layout's block granularity (16/32/64/128) — cost scales with the layout density.
-// Measured (tools/bench_flash_bwd.py, profiles/flash_bwd_bench_r2.jsonl): B8 H32 S4096 D128 causal 4.5 ms.
+// Measured (tools/bench_flash_bwd.py, profiles/flash_bwd_bench_r2_loaders.jsonl): B8 H32 S4096 D128 causal 4.44 ms.
+// Tried and measured slower: dQ partial stores + a summing pass instead of atomics (5.5 ms), pairing heavy and light
+// key blocks across XCDs for few-head long sequences (32k: 5.0 vs 4.75 ms; the dispatcher balances heavy-first).
 #include "ds_hip.h"
 
 #include <cstdlib>
@@ -174,12 +176,21 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
 
   // ------------------------------------------------------------------ staging of one (Q, dO, lse, delta) tile
   // by LDS-DMA, two tiles ahead of the one being computed (no staging registers, no wait until the barrier that
-  // precedes its use). Wave w fills the 1-KB pieces w (and w+8 when NW = 4) of the swizzled Q and dO images: lane L
-  // of piece j lands at physical chunk 64j + L, i.e. row 4j + L/16, physical chunk L%16, so it fetches the logical
-  // chunk (L%16) ^ swizzle(row) — the swizzle goes on the SOURCE address. Wave 0 also moves the 32 lse and 32 delta
-  // values (4 B per lane). Per tile a wave issues dma_ops() vector-memory instructions.
-  constexpr int PIECES = 8 / NW;  // 1-KB pieces of one 8-KB tile per wave
+  // precedes its use). Only the waves that issue no dQ atomics stage: `s_waitcnt vmcnt` counts loads, LDS-DMA and
+  // atomics together in issue order, so a wave that had its tile's 16 dQ atomics in flight ahead of its next DMA
+  // would have to wait for those memory-side atomics to retire (thousands of cycles with every CU adding) before
+  // the barrier that publishes the DMA — and every wave of the workgroup waits at that barrier. With the staging on
+  // the loader waves the atomics of waves 0..3 are never waited on inside the loop (they drain in the background,
+  // the hardware's outstanding-request limit is the only back-pressure).
+  // Loader wave lw fills the 1-KB pieces lw + 4i of the swizzled Q and dO images: lane L of piece j lands at physical
+  // chunk 64j + L, i.e. row 4j + L/16, physical chunk L%16, so it fetches the logical chunk (L%16) ^ swizzle(row) —
+  // the swizzle goes on the SOURCE address. Loader 0 also moves the 32 lse and 32 delta values (4 B per lane).
+  static_assert(NW == 8, "the loader / dQ wave split assumes 8 waves");
+  constexpr int NLOAD = 4, LPIECES = 8 / NLOAD;  // loader waves 4..7, 1-KB pieces of one 8-KB tile per loader
+  const bool loader = w >= NW - NLOAD;
+  const int lw = w - (NW - NLOAD);
   auto stage = [&](int it, int buf) {
+    if (!loader) return;
     int hq, qt;
     tile_at(it, hq, qt);
     int lane = threadIdx.x & 63;  // re-derived (and laundered) here: hoisted lane values were spilled
@@ -187,30 +198,27 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
     const bf16* qb = a.q + b * a.qsb + hq * a.qsh;
     const bf16* ob = a.dout + b * a.osb + hq * a.osh;
 #pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      const int j = w + i * NW, row = 4 * j + (lane >> 4), pch = lane & 15;
+    for (int i = 0; i < LPIECES; ++i) {
+      const int j = lw + i * NLOAD, row = 4 * j + (lane >> 4), pch = lane & 15;
       const int ch = pch ^ (((row & 3) << 2) | ((row >> 2) & 3));
       const int64_t qr = min(qt * QT + row, S - 1);
       glds16(qb + qr * a.qss + ch * 8, QD + buf * 2 * TILE + 1024 * j);
       glds16(ob + qr * a.oss + ch * 8, QD + buf * 2 * TILE + TILE + 1024 * j);
     }
-    if (w == 0) {
+    if (lw == 0) {
       const int r = min(qt * QT + (lane & 31), S - 1);
       const int64_t idx = ((int64_t)b * a.Hq + hq) * S + r;
       glds4(lane < 32 ? (const void*)(a.lse + idx) : (const void*)(a.delta + idx), (const char*)(LD + buf * 64));
     }
   };
-  // s_waitcnt vmcnt(N) with N = the DMA instructions this wave issued for the newest tile (so the older tile has
-  // landed), then lgkmcnt(0) (this wave's LDS writes done) and the raw barrier (no vmcnt(0) drain)
+  // loaders: s_waitcnt vmcnt(N) with N = the DMA instructions they issued for the newest tile (so the older tile has
+  // landed); everyone: lgkmcnt(0) (this wave's LDS writes done) and the raw barrier (no vmcnt(0) drain)
   auto barrier_keep_newest = [&](bool newest_in_flight) {
-    if (newest_in_flight) {
-      if (w == 0) {
-        if (PIECES == 1) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      } else {
-        if (PIECES == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      }
+    if (!loader) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (newest_in_flight) {
+      if (lw == 0) asm volatile("s_waitcnt vmcnt(5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }

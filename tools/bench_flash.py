@@ -25,7 +25,7 @@ def timeit(fn, iters=20):
     return a.elapsed_time(b) / iters
 
 
-for (B, H, S) in [(4, 32, 4096), (8, 32, 4096), (1, 32, 16384)]:
+for (B, H, S) in [(4, 32, 4096), (8, 32, 4096), (1, 32, 16384), (1, 4, 32768)]:
     for causal in (True, False):
         q, k, v = (torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16) for _ in range(3))
         scale = 1 / math.sqrt(128)
