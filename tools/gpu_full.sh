@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() { local t=$1; shift; echo "=== $* (limit ${t}s)"; timeout -k 10 "$t" "$@"; local rc=$?; echo "=== rc=$rc"; return $rc; }
-step 900 python -m pytest tests/unit/ops tests/unit/inference tests/unit/runtime tests/unit/moe tests/unit/pipe tests/unit/sequence tests/unit/hybrid_engine tests/unit/compression -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || exit 1
+step 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || exit 1
 step 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
 step 900 python bench.py --steps ${STEPS:-5} --warmup 2 > gpurun_out/bench_7b.log 2>&1 || exit 1
 echo "chain ok"
