@@ -576,6 +576,10 @@ class DeepSpeedEngine(nn.Module):
                 self.monitor.write_events(ev)
             if self.global_steps % self.steps_per_print() == 0 and self.global_rank == 0:
                 log_dist(f"step={self.global_steps}, skipped={self.skipped_steps}, lr={self.get_lr()}", ranks=[0])
+            if self.global_steps % self.steps_per_print() == 0 and self.wall_clock_breakdown() and \
+                    self.optimizer is not None and self.optimizer.coordinator is not None:
+                self.optimizer.coordinator.profiler.log_events()
+                self.optimizer.coordinator.profiler.reset_events()
             if self._fault_injector is not None:
                 self._fault_injector.on_step(self.global_steps)
         self.micro_steps += 1

@@ -36,6 +36,8 @@ class ParamCoordinator:
         self.max_live = int(max_live_parameters)
         self.max_reuse = int(max_reuse_distance)
         self._reuse_dist = []  # per trace position: gathered elements until the same group's next fetch (or None)
+        from .partitioned_param_profiler import PartitionedParameterProfiler
+        self.profiler = PartitionedParameterProfiler(getattr(opt, "timers", None))
         self.trace = []
         self.mode = RECORD
         self.pos = 0
@@ -115,6 +117,7 @@ class ParamCoordinator:
             return  # activation-checkpoint recompute inside backward: keep params for the module's backward
         g = m._ds_fetch_group
         if self._keep_for_reuse(g):
+            self.profiler.count("reuse_hit", g.numel)
             return
         self.release(g)
 
@@ -179,6 +182,7 @@ class ParamCoordinator:
             g.ag_event = None
         g.status = ZeroParamStatus.INFLIGHT
         self.live_numel += g.padded
+        self.profiler.count("all_gather", g.padded)
 
     def _wait(self, g):
         if g.status == ZeroParamStatus.INFLIGHT:
@@ -191,6 +195,7 @@ class ParamCoordinator:
 
     @instrument_w_nvtx
     def fetch(self, g):
+        self.profiler.count("fetch", g.numel)
         self._trace(g)
         if g.status == ZeroParamStatus.NOT_AVAILABLE:
             self._issue(g)
@@ -206,6 +211,7 @@ class ParamCoordinator:
         self.opt._release_params(g)
         g.full = None
         self.live_numel -= g.padded
+        self.profiler.count("release", g.numel)
 
     def release_after_backward(self, g):
         self.release(g)

@@ -189,7 +189,8 @@ def _reuse_run(reuse, out):
         per_step.append(gathers[0] - before)
     if rank == 0:
         torch.save({"losses": losses, "gathers": per_step, "n_groups": sum(not g.persistent
-                                                                            for g in eng.optimizer.groups)}, out)
+                                                                            for g in eng.optimizer.groups),
+                    "events": {k: list(v) for k, v in coord.profiler.summary().items()}}, out)
 
 
 def test_zero3_reuse_distance_skips_backward_gathers(tmp_path):
@@ -205,3 +206,5 @@ def test_zero3_reuse_distance_skips_backward_gathers(tmp_path):
     assert res[0]["gathers"][1:] == [2 * n] * 3
     assert res[int(1e10)]["gathers"][1:] == [n] * 3
     assert res[0]["losses"] == res[int(1e10)]["losses"]
+    # the coordinator's event profiler saw the retained groups (reference partitioned_param_profiler counters)
+    assert res[int(1e10)]["events"]["reuse_hit"][0] == 3 * n and "reuse_hit" not in res[0]["events"]
