@@ -80,6 +80,38 @@ __global__ void __launch_bounds__(256) rms_fwd_kernel(const T* __restrict__ x, c
 
 // ------------------------------------------------------------------------------------------------ RMSNorm bwd
 // x is the normalized input (x + r when the forward fused the residual). dx (+ dres if given).
+// One wave per row. The row's x and dy are read from HBM ONCE and kept in registers in their storage type (bf16: 4
+// VGPRs per 8 elements) across the two passes (dot product, then dx): re-reading them in the second pass missed
+// the 4 MB per-XCD L2 (512 rows in flight per XCD x 16 KB) and cost ~25 % extra traffic.
+template <typename T> struct Raw8 { typedef bf16x8 type; };
+template <> struct Raw8<fp16> { typedef fp16x8 type; };
+template <> struct Raw8<float> { struct type { f32x4 lo, hi; }; };
+template <typename T> __device__ __forceinline__ typename Raw8<T>::type ld_raw8(const T* p) {
+  return *reinterpret_cast<const typename Raw8<T>::type*>(p);
+}
+template <typename T> __device__ __forceinline__ void raw_to_f(const typename Raw8<T>::type& r, float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)r[i];
+}
+template <> __device__ __forceinline__ void raw_to_f<float>(const Raw8<float>::type& r, float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[i] = r.lo[i]; v[i + 4] = r.hi[i]; }
+}
+
+typedef unsigned int raw_u32x4 __attribute__((ext_vector_type(4)));
+template <typename T, int NV>
+__device__ __forceinline__ void launder_raw(typename Raw8<T>::type (&a)[NV], typename Raw8<T>::type (&b)[NV]) {
+  if constexpr (sizeof(typename Raw8<T>::type) == 16) {  // bf16 / fp16 rows (fp32 rows are not register-bound)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      raw_u32x4 ua = __builtin_bit_cast(raw_u32x4, a[k]), ub = __builtin_bit_cast(raw_u32x4, b[k]);
+      asm volatile("" : "+v"(ua), "+v"(ub));
+      a[k] = __builtin_bit_cast(typename Raw8<T>::type, ua);
+      b[k] = __builtin_bit_cast(typename Raw8<T>::type, ub);
+    }
+  }
+}
+
 template <typename T, int NV, bool ADD_DRES>
 __global__ void __launch_bounds__(256) rms_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const T* __restrict__ w, const float* __restrict__ rstd,
@@ -95,14 +127,24 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const T* __restrict__ dy, 
     const float rs = rstd[row];
     const T* xr = x + row * H;
     const T* gr = dy + row * H;
+    typename Raw8<T>::type xraw[NV], graw[NV], draw[ADD_DRES ? NV : 1];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        xraw[k] = ld_raw8(xr + c);
+        graw[k] = ld_raw8(gr + c);
+        if constexpr (ADD_DRES) draw[k] = ld_raw8(dres + row * H + c);  // in flight with x / dy, not after the dot
+      }
+    }
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 8;
       if (c < H) {
         float xv[8], gv[8], ww[8];
-        Vec8<T>::load(xr + c, xv);
-        Vec8<T>::load(gr + c, gv);
+        raw_to_f<T>(xraw[k], xv);
+        raw_to_f<T>(graw[k], gv);
         Vec8<T>::load(w + c, ww);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -113,19 +155,22 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const T* __restrict__ dy, 
     }
     dot = wave_sum(dot);
     const float c2 = dot * rs * rs * rs / H;
+    // opaque to the optimiser: the second pass re-converts from the packed registers instead of keeping the first
+    // pass's fp32 copies alive (that doubles the live registers and drops occupancy to 1 wave per SIMD)
+    launder_raw<T, NV>(xraw, graw);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 8;
       if (c < H) {
         float xv[8], gv[8], ww[8], o[8];
-        Vec8<T>::load(xr + c, xv);
-        Vec8<T>::load(gr + c, gv);
+        raw_to_f<T>(xraw[k], xv);
+        raw_to_f<T>(graw[k], gv);
         Vec8<T>::load(w + c, ww);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = gv[j] * ww[j] * rs - xv[j] * c2;
-        if (ADD_DRES) {
+        if constexpr (ADD_DRES) {
           float d2[8];
-          Vec8<T>::load(dres + row * H + c, d2);
+          raw_to_f<T>(draw[k], d2);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += d2[j];
         }
