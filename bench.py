@@ -26,7 +26,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-13b", "tiny"])
+    ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-13b", "llama2-70b", "tiny"])
+    ap.add_argument("--zero-init", action="store_true", help="construct the model inside zero.Init (ZeRO-3, >1 rank)")
+    ap.add_argument("--offload-ratio", type=float, default=0.0,
+                    help="ZeRO-Offload++ Twin-Flow: fraction of the fp32 master / Adam state kept in pinned host "
+                         "memory and stepped by the native CPU Adam concurrently with the device Adam (BASELINE "
+                         "config 4: Llama-2-70B ZeRO-3 + Twin-Flow)")
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("DS_BENCH_MB", "8")))
     ap.add_argument("--gas", type=int, default=1)
@@ -92,7 +97,8 @@ def main():
     args = parse()
     import deepspeedsyclsupport_amd as ds
     from deepspeedsyclsupport_amd import comm as dist
-    from deepspeedsyclsupport_amd.models.llama import LlamaConfig, LlamaForCausalLM, llama2_7b_config, llama2_13b_config
+    from deepspeedsyclsupport_amd.models.llama import (LlamaConfig, LlamaForCausalLM, llama2_7b_config, llama2_13b_config,
+                                                       llama2_70b_config)
 
     ds.init_distributed(dist_backend="gloo" if args.host_dryrun else "nccl")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -119,6 +125,8 @@ def main():
         cfg = llama2_7b_config(max_position_embeddings=args.seq_len)
     elif args.model == "llama2-13b":
         cfg = llama2_13b_config(max_position_embeddings=args.seq_len)
+    elif args.model == "llama2-70b":
+        cfg = llama2_70b_config(max_position_embeddings=args.seq_len)
     else:
         cfg = LlamaConfig(vocab_size=32000, hidden_size=1024, intermediate_size=2816, num_hidden_layers=4,
                           num_attention_heads=8, max_position_embeddings=args.seq_len)
@@ -127,8 +135,13 @@ def main():
     # build directly on the GPU in bf16 (fast init; fp32 masters are created by the ZeRO optimizer)
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.bfloat16 if on_gpu else torch.float32)
-    with torch.device(dev):
-        model = LlamaForCausalLM(cfg)
+    if (args.zero_init or args.model == "llama2-70b") and args.stage == 3 and world > 1:
+        # built straight into ZeRO-3 partitions (zero.Init): 70B's 140 GB of bf16 weights never sit whole on a rank
+        with ds.zero.Init(dtype=torch.bfloat16 if on_gpu else torch.float32), torch.device(dev):
+            model = LlamaForCausalLM(cfg)
+    else:
+        with torch.device(dev):
+            model = LlamaForCausalLM(cfg)
     torch.set_default_dtype(prev)
     if args.ckpt:
         model.gradient_checkpointing_enable()
@@ -156,6 +169,9 @@ def main():
             "stage3_max_reuse_distance": int(1e10),
         },
     }
+    if args.offload_ratio > 0:
+        config["zero_optimization"]["offload_optimizer"] = {"device": "cpu", "pin_memory": True,
+                                                            "ratio": args.offload_ratio}
     assert world % args.sp == 0, "--sp must divide the number of ranks"
     dp = world // args.sp
     if args.sp > 1:
@@ -239,6 +255,7 @@ def main():
                 # True when parameters / gradients really are partitioned and gathered / reduce-scattered in the
                 # timed steps (always with > 1 data-parallel rank; at one rank only with DS_ZERO_FORCE_PARTITION=1)
                 "zero_partitioned": bool(getattr(engine.optimizer, "partition", False)),
+                "twin_flow_offload_ratio": args.offload_ratio,
                 "attention": "in-tree CDNA4 flash fwd+bwd (csrc/attn/flash_{fwd,bwd}.hip)",
                 "micro_batch_per_gpu": args.micro_batch,
                 "gradient_accumulation_steps": args.gas,

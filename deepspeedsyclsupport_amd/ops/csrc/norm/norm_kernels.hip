@@ -293,18 +293,39 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
   for (int k = 0; k < NV; ++k) { zero8(dg[k]); zero8(db[k]); }
   const int64_t wstride = (int64_t)gridDim.x * 4;
+  // rows up to 2048 wide (BERT / GPT-2 class) stay in packed registers between the two passes like rms_bwd; wider
+  // rows re-read (their dgamma / dbeta accumulators already hold 128 registers)
+  constexpr bool KEEP = NV <= 4;
+  constexpr int NK = KEEP ? NV : 1;
   for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += wstride) {
     const float mu = mean[row], rs = rstd[row];
     const T* xr = x + row * H;
     const T* gr = dy + row * H;
+    typename Raw8<T>::type xraw[NK], graw[NK], draw[(KEEP && ADD_DRES) ? NK : 1];
+    if constexpr (KEEP) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < H) {
+          xraw[k] = ld_raw8(xr + c);
+          graw[k] = ld_raw8(gr + c);
+          if constexpr (ADD_DRES) draw[k] = ld_raw8(dres + row * H + c);
+        }
+      }
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 8;
       if (c < H) {
         float xv[8], gv[8], gm[8];
-        Vec8<T>::load(xr + c, xv);
-        Vec8<T>::load(gr + c, gv);
+        if constexpr (KEEP) {
+          raw_to_f<T>(xraw[k < NK ? k : 0], xv);
+          raw_to_f<T>(graw[k < NK ? k : 0], gv);
+        } else {
+          Vec8<T>::load(xr + c, xv);
+          Vec8<T>::load(gr + c, gv);
+        }
         Vec8<T>::load(gamma + c, gm);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -319,19 +340,26 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
     }
     s1 = wave_sum(s1) / H;
     s2 = wave_sum(s2) / H;
+    if constexpr (KEEP) launder_raw<T, NK>(xraw, graw);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 8;
       if (c < H) {
         float xv[8], gv[8], gm[8], o[8];
-        Vec8<T>::load(xr + c, xv);
-        Vec8<T>::load(gr + c, gv);
+        if constexpr (KEEP) {
+          raw_to_f<T>(xraw[k < NK ? k : 0], xv);
+          raw_to_f<T>(graw[k < NK ? k : 0], gv);
+        } else {
+          Vec8<T>::load(xr + c, xv);
+          Vec8<T>::load(gr + c, gv);
+        }
         Vec8<T>::load(gamma + c, gm);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rs * (gv[j] * gm[j] - s1 - (xv[j] - mu) * rs * s2);
         if (ADD_DRES) {
           float d2[8];
-          Vec8<T>::load(dres + row * H + c, d2);
+          if constexpr (KEEP) raw_to_f<T>(draw[k < NK ? k : 0], d2);
+          else Vec8<T>::load(dres + row * H + c, d2);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += d2[j];
         }

@@ -20,7 +20,8 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("extra", [[], ["--sp", "2"]], ids=["dp2", "sp2"])
+@pytest.mark.parametrize("extra", [[], ["--sp", "2"], ["--zero-init", "--offload-ratio", "0.5"]],
+                         ids=["dp2", "sp2", "zeroinit-twinflow"])
 def test_bench_two_rank_dryrun_prints_one_json_line(extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
@@ -34,7 +35,7 @@ def test_bench_two_rank_dryrun_prints_one_json_line(extra):
     assert KEYS <= set(rec), sorted(KEYS - set(rec))
     assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
     assert rec["value"] > 0 and rec["higher_is_better"] is True
-    assert rec["config"]["parallelism"] == ("dp1-sp2" if extra else "dp2")
+    assert rec["config"]["parallelism"] == ("dp1-sp2" if "--sp" in extra else "dp2")
     assert rec["final_loss"] == rec["final_loss"]  # not NaN
 
 
