@@ -247,7 +247,8 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (uniform random token ids, random-init weights)",
             "config": {
-                "model": {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "tiny": "llama-tiny"}[args.model],
+                "model": {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "llama2-70b": "Llama-2-70B",
+                          "tiny": "llama-tiny"}[args.model],
                 "global_batch": dp * args.micro_batch * args.gas,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{dp}" + (f"-sp{args.sp}" if args.sp > 1 else ""),
