@@ -137,3 +137,30 @@ def test_moe_expert_grad_scaling_switch(tmp_path):
         else:
             torch.testing.assert_close(h, g)
     assert n_exp > 0
+
+
+def _prmoe(out):
+    from deepspeedsyclsupport_amd.moe.layer import MoE
+    torch.manual_seed(0)
+    H = 8
+    expert = torch.nn.Sequential(torch.nn.Linear(H, 16), torch.nn.ReLU(), torch.nn.Linear(16, H))
+    layer = MoE(H, expert, num_experts=2, ep_size=1, k=1, use_residual=True, min_capacity=16)
+    x = torch.randn(12, H, requires_grad=True)
+    y, l_aux, counts = layer(x)
+    with torch.no_grad():
+        moe_out = layer.deepspeed_moe(x)
+        coef = torch.softmax(layer.coefficient(x), dim=-1)
+        want = moe_out * coef[:, :1] + layer.mlp(x) * coef[:, 1:]
+    y.sum().backward()
+    torch.save({"y": y.detach(), "want": want, "coef_grad": layer.coefficient.weight.grad is not None,
+                "mlp_grad": layer.mlp[0].weight.grad is not None}, out)
+
+
+def test_residual_moe_combines_expert_and_dense_paths(tmp_path):
+    """PR-MoE (`use_residual=True`, reference `moe/layer.py:77-80,115-124`): output = softmax-gated mix of the routed
+    expert output and a dense MLP, both trained."""
+    out = str(tmp_path / "p.pt")
+    run_distributed(_prmoe, 1, out)
+    d = torch.load(out, weights_only=True)
+    torch.testing.assert_close(d["y"], d["want"], rtol=1e-5, atol=1e-6)
+    assert d["coef_grad"] and d["mlp_grad"]

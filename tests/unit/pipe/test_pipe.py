@@ -104,3 +104,45 @@ def test_topology_radix_math():
     assert topo.filter_match(pipe=1, model=0) == [r for c, r in brute.items() if c[0] == 1 and c[2] == 0]
     assert topo.get_rank_repr(5) == "model_01"
     assert ProcessTopology(["a"], [4]).get_axis_comm_lists("b") == []
+
+
+def _tied_specs():
+    from deepspeedsyclsupport_amd.pipe import LayerSpec, TiedLayerSpec
+    # the same [H, H] matrix is the input projection (x W^T) on the first stage and the transposed output projection
+    # (x W) on the last stage: the reference's tied embedding / LM head pattern (`tests/unit/pipe/test_pipe_module.py`)
+    return ([TiedLayerSpec("tied", nn.Linear, H, H, bias=False)] +
+            [LayerSpec(nn.Sequential, nn.Linear(H, H), nn.Tanh()) for _ in range(4)] +
+            [TiedLayerSpec("tied", nn.Linear, H, H, bias=False, forward_fn=lambda m, x: x @ m.weight),
+             LayerSpec(nn.Linear, H, 4)])
+
+
+def _tied_run(stages, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.pipe import PipelineModule
+    net = PipelineModule(layers=_tied_specs(), num_stages=stages, loss_fn=nn.functional.cross_entropy,
+                         partition_method="uniform", seed_layers=True)
+    cfg = {"train_micro_batch_size_per_gpu": MB, "gradient_accumulation_steps": M,
+           "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.01}}, "steps_per_print": 1000}
+    eng, _, _, _ = ds.initialize(model=net, config=cfg)
+    it = iter(_data())
+    losses = [float(eng.train_batch(it)) for _ in range(STEPS)]
+    tied = [w.detach().clone() for w, _ in net.get_tied_weights_and_groups()] if hasattr(
+        net, "get_tied_weights_and_groups") else []
+    gathered = [None] * dist.get_world_size()
+    dist.all_gather_object(gathered, [t.sum().item() for t in tied])
+    if dist.get_rank() == 0:
+        torch.save({"losses": losses, "tied": gathered}, out)
+
+
+def test_pipe_tied_layers_match_single_stage(tmp_path):
+    """TiedLayerSpec across the first and last stage: copies start equal (broadcast), their gradients are
+    all-reduced over the tie group every step, so 2 stages train exactly like 1 stage holding one shared module."""
+    res = {}
+    for stages in (1, 2):
+        out = str(tmp_path / f"t{stages}.pt")
+        run_distributed(_tied_run, stages, stages, out)
+        res[stages] = torch.load(out)
+    assert res[2]["losses"] == pytest.approx(res[1]["losses"], rel=1e-4, abs=1e-5)
+    t = res[2]["tied"]
+    assert len(t) == 2 and t[0] and t[0] == pytest.approx(t[1], rel=1e-6)
