@@ -52,6 +52,7 @@ constexpr int lds_bytes() { return K_BYTES + NBUF * 2 * TILE + 2 * DS_BYTES + NB
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -93,6 +94,13 @@ __device__ __forceinline__ int lds_off(int row, int ch) {
 // dS^T image: 64-B rows (32 queries), 8-B unit u (4 queries) XOR-swizzled by (key >> 1) & 7 so that 16 lanes storing
 // one unit of 16 consecutive keys hit 32 distinct banks.
 __device__ __forceinline__ int ds_off(int key, int u) { return key * 64 + 8 * (u ^ ((key >> 1) & 7)); }
+
+// two fp32 -> one dword of two bf16 (round to nearest even), lo in bits 0..15
+__device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
 
 // row of a 32x32 accumulator register r for lane half h
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
@@ -367,14 +375,37 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[c][kk], dp, 0, 0, 0);
       }
       // ---------------- P and dS, dS^T -> LDS (row = key, 8-B unit g*2+h holds queries 8g+4h .. +3)
-      bf16x8_t pb[2], dsb[2];
+      // P and dS in fp32, then packed two per instruction (v_cvt_pk_bf16_f32; hipcc lowers a vector fptrunc to one
+      // convert + v_perm per element). Masking only when some lane of the wave needs it (diagonal / padded tiles):
+      // the per-element select costs 4 VALU and the VALU issue slots are the co-bottleneck beside the MFMAs.
+      float pf[16], df[16];
       const bool need_mask = keep[c] != 0xffffu;
+      if (__any(need_mask)) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = __builtin_amdgcn_exp2f(s[r] * a.c);
-        if (need_mask && !((keep[c] >> r) & 1u)) p = 0.f;
-        pb[r >> 3][r & 7] = (bf16)p;
-        dsb[r >> 3][r & 7] = (bf16)(p * dp[r]);
+        for (int r = 0; r < 16; ++r) {
+          float p = __builtin_amdgcn_exp2f(s[r] * a.c);
+          if (!((keep[c] >> r) & 1u)) p = 0.f;
+          pf[r] = p;
+          df[r] = p * dp[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          pf[r] = __builtin_amdgcn_exp2f(s[r] * a.c);
+          df[r] = pf[r] * dp[r];
+        }
+      }
+      bf16x8_t pb[2], dsb[2];
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        u32x4_t pu, du;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pu[i] = pack_bf16(pf[8 * g + 2 * i], pf[8 * g + 2 * i + 1]);
+          du[i] = pack_bf16(df[8 * g + 2 * i], df[8 * g + 2 * i + 1]);
+        }
+        pb[g] = __builtin_bit_cast(bf16x8_t, pu);
+        dsb[g] = __builtin_bit_cast(bf16x8_t, du);
       }
       char* dsw = DSc + (KPW * w + 32 * c) * 64;
 #pragma unroll
@@ -388,16 +419,29 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
         *reinterpret_cast<s16x4*>(dsw + dwbase + 16 * (g ^ dwtog)) = v4;
       }
       // ---------------- dV^T += dO^T.P, dK^T += Q^T.dS   (A operands by transposed reads of the tile images)
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        if (a.dbg & 4) break;
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
+      // 16 MFMAs, i = (dt, s2, O|Q). The transposed reads of operand i+2 are issued before MFMA i and the order is
+      // pinned with sched_barrier (ALU may cross, MFMA / LDS may not; a full barrier hits a hipcc ROCm 7.2 codegen
+      // error): left to itself the scheduler reused one operand quad and waited lgkmcnt(0) in front of every MFMA
+      // (LDS latency fully exposed; SQ_VALU_MFMA_BUSY_CYCLES put the kernel at ~29 % MFMA utilisation).
+      if (!(a.dbg & 4)) {
+        auto opnd = [&](int i) {
+          const int dt = i >> 2, s2 = (i >> 1) & 1;
+          const char* base = Qt + ((i & 1) ? 0 : TILE) + 4096 * s2;  // Ot = Qt + TILE (integer select)
           const int t0a = tbase[0] + 64 * (dt ^ ttog[0]), t1a = tbase[1] + 64 * (dt ^ ttog[1]);
-          const bf16x8_t oT = join(tr_read(Ot + 4096 * s2 + t0a), tr_read(Ot + 4096 * s2 + t1a));
-          dv[c][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oT, pb[s2], dv[c][dt], 0, 0, 0);
-          const bf16x8_t qT = join(tr_read(Qt + 4096 * s2 + t0a), tr_read(Qt + 4096 * s2 + t1a));
-          dk[c][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, dsb[s2], dk[c][dt], 0, 0, 0);
+          return join(tr_read(base + t0a), tr_read(base + t1a));
+        };
+        bf16x8_t o0 = opnd(0), o1 = opnd(1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          bf16x8_t o2;
+          if (i + 2 < 16) o2 = opnd(i + 2);
+          __builtin_amdgcn_sched_barrier(0x7);
+          const int dt = i >> 2, s2 = (i >> 1) & 1;
+          if (i & 1) dk[c][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o0, dsb[s2], dk[c][dt], 0, 0, 0);
+          else dv[c][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o0, pb[s2], dv[c][dt], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0x7);
+          o0 = o1;
+          o1 = o2;
         }
       }
     }

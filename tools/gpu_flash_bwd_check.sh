@@ -4,5 +4,5 @@ mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 300 python -u -m pytest tests/unit/ops/test_flash_attn_gpu.py tests/unit/ops/sparse_attention -x -q --timeout 120 --timeout-method thread > gpurun_out/fb_tests.log 2>&1 &&
 timeout -k 10 300 python tools/bench_flash_bwd.py > gpurun_out/fb_bench.log 2>&1 &&
-timeout -k 10 300 python tools/bench_flash.py > gpurun_out/ff_bench.log 2>&1
+timeout -k 10 200 python tools/flash_bwd_ablate.py > gpurun_out/ablate.log 2>&1
 echo rc=$?
