@@ -231,7 +231,6 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
   };
-  const float inv_scale = 1.f / a.scale;
 
   // ------------------------------------------------------------------ resident K image + per-wave V fragments
   for (int i = tid; i < KB * 16; i += NTHR) {
@@ -360,7 +359,7 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
         const f32x4 x = *reinterpret_cast<const f32x4*>(lse2 + 8 * g + 4 * h);
         const f32x4 y = *reinterpret_cast<const f32x4*>(dlt + 8 * g + 4 * h);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { s[4 * g + i] = -x[i] * inv_scale; dp[4 * g + i] = -y[i]; }
+        for (int i = 0; i < 4; ++i) { s[4 * g + i] = x[i]; dp[4 * g + i] = y[i]; }
       }
       const char* Kc = Kimg + (KPW * w + 32 * c) * 256;
 #pragma unroll
@@ -538,11 +537,14 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
   }
 }
 
-// delta[b,h,q] = sum_d O*dO (fp32), and zero the dQ accumulator row. 16 threads per row, 8 elements each.
+// Row constants of the main kernel's accumulator initialisation, pre-negated / pre-scaled so the main loop spends
+// no VALU on them: nrow[row] = -sum_d O*dO (-delta), nrow[rows + row] = -LSE / scale. Also zeroes the dQ accumulator
+// row. 16 threads per row, 8 elements each.
 __global__ void __launch_bounds__(256) flash_bwd_pre_kernel(const bf16* __restrict__ O, const bf16* __restrict__ dO,
-                                                            float* __restrict__ delta, float* __restrict__ dqacc,
-                                                            int Hq, int S, int64_t rows, int64_t osb, int64_t osh,
-                                                            int64_t oss, int64_t gsb, int64_t gsh, int64_t gss) {
+                                                            const float* __restrict__ lse, float* __restrict__ nrow,
+                                                            float* __restrict__ dqacc, int Hq, int S, int64_t rows,
+                                                            int64_t osb, int64_t osh, int64_t oss, int64_t gsb,
+                                                            int64_t gsh, int64_t gss, float inv_scale) {
   const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int sub = threadIdx.x & 15;
   if (row >= rows) return;
@@ -557,7 +559,10 @@ __global__ void __launch_bounds__(256) flash_bwd_pre_kernel(const bf16* __restri
   for (int i = 0; i < 8; ++i) acc = fmaf((float)o[i], (float)g[i], acc);
 #pragma unroll
   for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
-  if (sub == 0) delta[row] = acc;
+  if (sub == 0) {
+    nrow[row] = -acc;
+    nrow[rows + row] = -lse[row] * inv_scale;
+  }
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   *reinterpret_cast<f32x4*>(dqacc + row * D + sub * 8) = z;
   *reinterpret_cast<f32x4*>(dqacc + row * D + sub * 8 + 4) = z;
@@ -610,7 +615,8 @@ int launch_mode(const BwdArgs& a, int mode, hipStream_t st) {
 
 // Strides are (batch, head, seq) in elements, unit last stride everywhere, all bf16 rows 16-B aligned.
 // q/o/dout/dq [B,Hq,S,128], k/v/dk/dv [B,Hk,S,128], lse [B,Hq,S] natural-log (flash_fwd's), workspace:
-// delta [B*Hq*S] fp32 and dqacc [B*Hq*S*128] fp32. mode: 0 full, 1 causal (top-left), 2 block-sparse (LUT below).
+// delta [2*B*Hq*S] fp32 (the pre kernel's -delta and -LSE/scale rows) and dqacc [B*Hq*S*128] fp32.
+// mode: 0 full, 1 causal (top-left), 2 block-sparse (LUT below).
 extern "C" int ds_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                             const float* lse, float* delta, float* dqacc, void* dq, void* dk, void* dv, int B, int Hq,
                             int Hk, int S, const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os,
@@ -623,12 +629,12 @@ extern "C" int ds_flash_bwd(const void* q, const void* k, const void* v, const v
     return (int)hipErrorInvalidValue;
   const int64_t rows = (int64_t)B * Hq * S;
   const int pgrid = (int)((rows + 15) / 16);
-  hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3(pgrid), dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta,
-                     dqacc, Hq, S, rows, os[0], os[1], os[2], dos[0], dos[1], dos[2]);
+  hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3(pgrid), dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, lse,
+                     delta, dqacc, Hq, S, rows, os[0], os[1], os[2], dos[0], dos[1], dos[2], 1.f / scale);
   DS_CHECK_LAUNCH();
   BwdArgs a;
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.dout = (const bf16*)dout;
-  a.lse = lse; a.delta = delta; a.dqacc = dqacc; a.dk = (bf16*)dk; a.dv = (bf16*)dv;
+  a.lse = delta + rows; a.delta = delta; a.dqacc = dqacc; a.dk = (bf16*)dk; a.dv = (bf16*)dv;  // pre-kernel rows
   a.B = B; a.Hq = Hq; a.Hk = Hk; a.S = S;
   a.qsb = qs[0]; a.qsh = qs[1]; a.qss = qs[2];
   a.ksb = ks[0]; a.ksh = ks[1]; a.kss = ks[2];

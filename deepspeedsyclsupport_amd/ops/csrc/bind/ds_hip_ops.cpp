@@ -552,7 +552,7 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse
   }
   auto mk = [&](int64_t H) { return torch::empty({B, S, H, 128}, q.options()).transpose(1, 2); };
   auto dq = mk(Hq), dk = mk(Hk), dv = mk(Hk);
-  auto delta = torch::empty({B * Hq * S}, q.options().dtype(at::kFloat));
+  auto delta = torch::empty({2 * B * Hq * S}, q.options().dtype(at::kFloat));  // -delta and -LSE/scale rows
   auto dqacc = torch::empty({B * Hq * S * 128}, q.options().dtype(at::kFloat));
   auto st3 = [](const Tensor& t, int64_t* s) { for (int d = 0; d < 3; ++d) s[d] = t.stride(d); };
   int64_t qs[3], ks[3], vs[3], os[3], gs[3], dqs[3], dks[3], dvs[3];
