@@ -31,7 +31,9 @@
 //    reuse in L2);
 //  * block-sparse: each workgroup walks only the 32-row query tiles its key block meets in the layout (a host-built
 //    column LUT) and masks at the layout's block granularity (16/32/64/128) — cost scales with the layout density.
-// Measured (tools/bench_flash_bwd.py, profiles/flash_bwd_bench_r2_loaders.jsonl): B8 H32 S4096 D128 causal 4.44 ms.
+// Measured (tools/bench_flash_bwd.py, profiles/flash_bwd_bench_r2_final.jsonl): B8 H32 S4096 D128 causal 4.2-4.3 ms
+// (round-2 start: 4.58). SQ PMC of the round-2 start: ~29 % MFMA busy, ~9 VALU per MFMA -- the VALU issue slots, not
+// the matrix pipe, are what the trims above (packed converts, pre-scaled row constants, uniform mask skip) buy back.
 // Tried and measured slower: dQ partial stores + a summing pass instead of atomics (5.5 ms), pairing heavy and light
 // key blocks across XCDs for few-head long sequences (32k: 5.0 vs 4.75 ms; the dispatcher balances heavy-first).
 #include "ds_hip.h"
@@ -502,12 +504,14 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
         int ln = threadIdx.x;
         asm volatile("" : "+v"(ln));
         const int lofs = 4 * ((ln >> 5) & 1) * D + 32 * ((ln >> 6) & 3) + (ln & 31);
-        float* dqp = a.dqacc + (((int64_t)b * a.Hq + hq) * S + q0) * D + lofs;
+        // wave-uniform 64-bit base (scalar registers) + 32-bit per-lane element offset: the atomics take the
+        // saddr form instead of a 64-bit VGPR address built with an add/addc pair per atomic
+        float* dqb = a.dqacc + (((int64_t)b * a.Hq + hq) * S + q0) * D;
         const int lim = S - q0 - 4 * ((ln >> 5) & 1);  // rows (r&3) + 8(r>>2) below lim are inside the sequence
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qr = (r & 3) + 8 * (r >> 2);
-          if (qr < lim) unsafeAtomicAdd(dqp + qr * D, dq[r]);
+          if (qr < lim) unsafeAtomicAdd(dqb + (lofs + qr * D), dq[r]);
         }
       }
     }
