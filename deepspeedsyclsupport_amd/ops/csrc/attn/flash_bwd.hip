@@ -35,7 +35,9 @@
 // (round-2 start: 4.58). SQ PMC of the round-2 start: ~29 % MFMA busy, ~9 VALU per MFMA -- the VALU issue slots, not
 // the matrix pipe, are what the trims above (packed converts, pre-scaled row constants, uniform mask skip) buy back.
 // Tried and measured slower: dQ partial stores + a summing pass instead of atomics (5.5 ms), pairing heavy and light
-// key blocks across XCDs for few-head long sequences (32k: 5.0 vs 4.75 ms; the dispatcher balances heavy-first).
+// key blocks across XCDs for few-head long sequences (32k: 5.0 vs 4.75 ms; the dispatcher balances heavy-first),
+// splitting long key blocks' query ranges over several workgroups with fp32 dK/dV atomics (4 heads x 32k: 6.7 vs
+// 4.3 ms; +10 SGPR spills and the split bookkeeping slowed every shape).
 #include "ds_hip.h"
 
 #include <cstdlib>
