@@ -104,3 +104,17 @@ def test_layer_bf16_gpu_prefill_and_decode():
     for t in range(36, 40):
         out, past = gpu(x[:, t:t + 1].cuda().bfloat16(), layer_past=past, use_cache=True)
         torch.testing.assert_close(out[:, 0].float().cpu(), full[:, t], atol=5e-2, rtol=5e-2)
+
+
+def test_bloom_alibi_and_gqa_decode_consistency():
+    """ALiBi (bigscience_bloom) and grouped KV heads: cached decode reproduces the full-sequence forward."""
+    torch.manual_seed(4)
+    for kw in (dict(bigscience_bloom=True), dict(num_kv=2, rotary_dim=16, rotate_half=True)):
+        layer = DeepSpeedTransformerInference(_cfg(**kw), device="cpu")
+        x = torch.randn(1, 10, 64)
+        full = layer(x)[0]
+        out, past = layer(x[:, :7], use_cache=True)
+        assert past[0].shape[1] == (2 if "num_kv" in kw else 4)
+        for t in range(7, 10):
+            out, past = layer(x[:, t:t + 1], layer_past=past, use_cache=True)
+            torch.testing.assert_close(out[:, 0], full[:, t], atol=1e-5, rtol=1e-5)
