@@ -393,23 +393,6 @@ def open_source(ckpt_dir, mp_rank=0):
 
 
 # ---------------------------------------------------------------------------------------------------- restore
-class _NvmeStateCache:
-    """Write-back view of NVMe-swapped Twin-Flow moments: read each optimizer group once, scatter, write back."""
-
-    def __init__(self, swapper):
-        self.sw = swapper
-        self.cache = {}
-
-    def get(self, og):
-        if og not in self.cache:
-            self.cache[og] = list(self.sw.read_full(og))
-        return self.cache[og]
-
-    def flush(self):
-        for og, (m, v, st) in self.cache.items():
-            self.sw.write_full(og, m, v, st)
-
-
 @torch.no_grad()
 def restore_from_source(optimizer, module, source, load_optimizer_states=True, strict=True):
     """Scatter every parameter's fp32 master (and, when asked and present, Adam moments) from `source` into this
@@ -419,7 +402,6 @@ def restore_from_source(optimizer, module, source, load_optimizer_states=True, s
     want_moments = load_optimizer_states and source.has_moments()
     if want_moments:
         optimizer._ensure_state()
-    nvme = _NvmeStateCache(optimizer.nvme_swapper) if getattr(optimizer, "nvme_swapper", None) is not None else None
     missing = []
     for p in optimizer.opt_params:
         local = names.get(id(p))
@@ -430,30 +412,15 @@ def restore_from_source(optimizer, module, source, load_optimizer_states=True, s
         if v is None:
             missing.append(key)
             continue
-        optimizer._scatter_param(p, v, optimizer._state_src("fp32"), also_shard=True)
+        optimizer._scatter_param(p, v, "fp32", also_shard=True)
         if want_moments:
             for k in ("exp_avg", "exp_avg_sq"):
                 m = source.get(key, k)
-                if m is None:
-                    continue
-                fetch = optimizer._state_src(k)
-                if nvme is not None:
-                    base_fetch = fetch
-                    idx = {"exp_avg": 0, "exp_avg_sq": 1}[k]
-
-                    def fetch(og, on_host, _b=base_fetch, _i=idx):  # noqa: E731
-                        if on_host and og in nvme.sw.sizes:
-                            return nvme.get(og)[_i]
-                        return _b(og, on_host)
-                optimizer._scatter_param(p, m, fetch)
+                if m is not None:
+                    optimizer._scatter_param(p, m, k)
     if strict and missing:
         raise KeyError(f"checkpoint has no fp32 state for {len(missing)} parameter(s), e.g. {missing[:3]}")
     step = source.step() if want_moments else None
-    if nvme is not None:
-        if step is not None:
-            for og in nvme.cache:
-                nvme.cache[og][2] = step
-        nvme.flush()
     if step is not None:
         optimizer.set_step(step)
     optimizer._post_step_gather()

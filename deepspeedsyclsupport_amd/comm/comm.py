@@ -314,7 +314,6 @@ def inference_all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, **
     return tdist.all_reduce(tensor, op=op, group=group, async_op=async_op)
 
 
-@timed_op
 def has_all_reduce_coalesced():
     return hasattr(tdist, "all_reduce_coalesced")
 
@@ -327,6 +326,7 @@ def all_gather_coalesced(output_tensors, input_tensors, group=None, async_op=Fal
     return cm if async_op else None
 
 
+@timed_op
 def all_reduce_coalesced(tensors, op=ReduceOp.SUM, group=None, async_op=False, **kw):
     return tdist.all_reduce_coalesced(tensors, op=op, group=group, async_op=async_op)
 

@@ -14,6 +14,8 @@ int ds_adam_flat(void*, void*, void*, const void*, void*, int64_t, int, int, int
                  float, float, float, int, hipStream_t);
 int ds_adam_multi(void**, void**, void**, const void**, void**, const int64_t*, int, int, int, int, float, float,
                   float, float, float, float, float, float, int, hipStream_t);
+int ds_adam_multi_split(void**, void**, void**, const void**, void**, const int64_t*, int, int, float, float, float,
+                        float, float, float, float, float, int, hipStream_t);
 int ds_lion_flat(void*, void*, const void*, void*, int64_t, int, int, int, float, float, float, float, float,
                  hipStream_t);
 int ds_adagrad_flat(void*, void*, const void*, void*, int64_t, int, int, int, float, float, float, float, hipStream_t);
@@ -117,6 +119,33 @@ void adam_multi(std::vector<Tensor> p, std::vector<Tensor> m, std::vector<Tensor
   check(ds_adam_multi(pp.data(), mp.data(), vp.data(), gp.data(), lp.empty() ? nullptr : lpp.data(), nn.data(), (int)n,
                       pd, gd, ld, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, adamw ? 1 : 0, stream()),
         "adam_multi");
+}
+
+// split-master Adam: lo int16 residuals, m/v fp32, g any dtype, hi bf16 weights updated in place
+void adam_multi_split(std::vector<Tensor> lo, std::vector<Tensor> m, std::vector<Tensor> v, std::vector<Tensor> g,
+                      std::vector<Tensor> hi, double lr, double b1, double b2, double eps, double wd, double bc1,
+                      double bc2, double grad_scale, bool adamw) {
+  const size_t n = lo.size();
+  if (n == 0) return;
+  TORCH_CHECK(m.size() == n && v.size() == n && g.size() == n && hi.size() == n, "list sizes");
+  std::vector<void*> lp(n), mp(n), vp(n), hp(n);
+  std::vector<const void*> gp(n);
+  std::vector<int64_t> nn(n);
+  const int gd = dcode(g[0]);
+  for (size_t i = 0; i < n; ++i) {
+    need(lo[i], "lo"); need(m[i], "m"); need(v[i], "v"); need(g[i], "g"); need(hi[i], "hi");
+    TORCH_CHECK(lo[i].scalar_type() == at::kShort && hi[i].scalar_type() == at::kBFloat16 &&
+                m[i].scalar_type() == at::kFloat && v[i].scalar_type() == at::kFloat && dcode(g[i]) == gd,
+                "adam_multi_split: lo int16, hi bf16, m/v fp32, one grad dtype per call");
+    const int64_t k = lo[i].numel();
+    TORCH_CHECK(m[i].numel() == k && v[i].numel() == k && g[i].numel() == k && hi[i].numel() == k,
+                "adam_multi_split: size mismatch");
+    lp[i] = lo[i].data_ptr(); mp[i] = m[i].data_ptr(); vp[i] = v[i].data_ptr(); gp[i] = g[i].data_ptr();
+    hp[i] = hi[i].data_ptr(); nn[i] = k;
+  }
+  check(ds_adam_multi_split(lp.data(), mp.data(), vp.data(), gp.data(), hp.data(), nn.data(), (int)n, gd, lr, b1, b2,
+                            eps, wd, bc1, bc2, grad_scale, adamw ? 1 : 0, stream()),
+        "adam_multi_split");
 }
 
 void lion_flat(Tensor p, Tensor m, Tensor g, OptT lp, double lr, double b1, double b2, double wd, double grad_scale) {
@@ -583,6 +612,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "deepspeedsyclsupport_amd gfx950 kernels";
   m.def("adam_flat", &adam_flat);
   m.def("adam_multi", &adam_multi);
+  m.def("adam_multi_split", &adam_multi_split);
   m.def("lion_flat", &lion_flat);
   m.def("adagrad_flat", &adagrad_flat);
   m.def("lamb_flat", &lamb_flat);

@@ -231,6 +231,8 @@ int64_t deepspeed_memcpy(torch::Tensor dest, torch::Tensor src) {
 }
 
 void register_aio(pybind11::module& m) {
+  // blocking transfers and wait() run without the interpreter lock (other Python threads keep launching GPU work)
+  using nogil = pybind11::call_guard<pybind11::gil_scoped_release>;
   m.def("aio_read", &aio_read);
   m.def("aio_write", &aio_write);
   m.def("deepspeed_memcpy", &deepspeed_memcpy);
@@ -245,13 +247,13 @@ void register_aio(pybind11::module& m) {
       .def("get_thread_count", &AioHandle::get_thread_count)
       .def("read", [](AioHandle& h, torch::Tensor b, const std::string& f, bool validate) { return h.sync_pread(b, f); })
       .def("write", [](AioHandle& h, torch::Tensor b, const std::string& f, bool validate) { return h.sync_pwrite(b, f); })
-      .def("pread", &AioHandle::pread)
-      .def("pwrite", &AioHandle::pwrite)
-      .def("sync_pread", &AioHandle::sync_pread)
-      .def("sync_pwrite", &AioHandle::sync_pwrite)
-      .def("async_pread", &AioHandle::async_pread)
-      .def("async_pwrite", &AioHandle::async_pwrite)
+      .def("pread", &AioHandle::pread, nogil())
+      .def("pwrite", &AioHandle::pwrite, nogil())
+      .def("sync_pread", &AioHandle::sync_pread, nogil())
+      .def("sync_pwrite", &AioHandle::sync_pwrite, nogil())
+      .def("async_pread", &AioHandle::async_pread, nogil())
+      .def("async_pwrite", &AioHandle::async_pwrite, nogil())
       .def("new_cpu_locked_tensor", &AioHandle::new_cpu_locked_tensor)
       .def("free_cpu_locked_tensor", &AioHandle::free_cpu_locked_tensor)
-      .def("wait", &AioHandle::wait);
+      .def("wait", &AioHandle::wait, nogil());
 }

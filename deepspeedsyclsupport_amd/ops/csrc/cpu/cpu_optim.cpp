@@ -100,6 +100,66 @@ __attribute__((target_clones("avx512f", "avx2", "default"))) void cvt_bf16_tile(
   }
 }
 
+// Split-master tile: the fp32 master is (hi << 16) + sext(lo) with hi = the bf16 weight (round half away from zero)
+// and lo a signed 16-bit residual; `hi_out` may alias `g` (the pinned staging buffer receives the gradient and
+// returns the updated weight), which is safe because iteration i reads g[i] before it writes hi_out[i].
+template <typename TG>
+inline float grad_f32(const TG* g, int64_t i);
+template <>
+inline float grad_f32<float>(const float* g, int64_t i) { return g[i]; }
+template <>
+inline float grad_f32<uint16_t>(const uint16_t* g, int64_t i) {
+  uint32_t u = (uint32_t)g[i] << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+#define DS_SPLIT_TILE(NAME, TG)                                                                                      \
+  __attribute__((target_clones("avx512f", "avx2", "default"))) void NAME(                                           \
+      int16_t* __restrict__ lo, float* __restrict__ m, float* __restrict__ v, const TG* g,                           \
+      const uint16_t* __restrict__ hi_in, uint16_t* hi_out, int64_t n, float lr, float b1, float b2, float eps,      \
+      float wd, float step_size, float denom_scale, float gs, int adamw) {                                           \
+    _Pragma("omp simd") for (int64_t i = 0; i < n; ++i) {                                                            \
+      uint32_t u = ((uint32_t)hi_in[i] << 16) + (uint32_t)(int32_t)lo[i];                                            \
+      float p;                                                                                                       \
+      std::memcpy(&p, &u, 4);                                                                                        \
+      float gg = grad_f32<TG>(g, i) * gs;                                                                            \
+      if (!adamw) gg += wd * p;                                                                                      \
+      const float mm = b1 * m[i] + (1.f - b1) * gg;                                                                  \
+      const float vv = b2 * v[i] + (1.f - b2) * gg * gg;                                                             \
+      float upd = mm * step_size / (std::sqrt(vv) * denom_scale + eps);                                              \
+      if (adamw) upd += wd * p;                                                                                      \
+      p -= lr * upd;                                                                                                 \
+      m[i] = mm;                                                                                                     \
+      v[i] = vv;                                                                                                     \
+      std::memcpy(&u, &p, 4);                                                                                        \
+      hi_out[i] = (uint16_t)((u + 0x8000u) >> 16);                                                                   \
+      lo[i] = (int16_t)(u & 0xffffu);                                                                                \
+    }                                                                                                                \
+  }
+DS_SPLIT_TILE(adam_split_tile_bf16g, uint16_t)
+DS_SPLIT_TILE(adam_split_tile_f32g, float)
+
+__attribute__((target_clones("avx512f", "avx2", "default"))) void acc_tile_bf16(float* __restrict__ d,
+                                                                                const uint16_t* __restrict__ s,
+                                                                                int64_t n, float alpha, int first) {
+#pragma omp simd
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t u = (uint32_t)s[i] << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    d[i] = first ? f * alpha : d[i] + f * alpha;
+  }
+}
+__attribute__((target_clones("avx512f", "avx2", "default"))) double sumsq_tile(const float* __restrict__ s,
+                                                                               int64_t n) {
+  double acc = 0.0;
+#pragma omp simd reduction(+ : acc)
+  for (int64_t i = 0; i < n; ++i) acc += (double)s[i] * (double)s[i];
+  return acc;
+}
+
 void check_host(const torch::Tensor& t, const char* n) {
   TORCH_CHECK(t.device().is_cpu() && t.is_contiguous(), n, " must be a contiguous host tensor");
 }
@@ -157,6 +217,73 @@ void cpu_adam_update(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::T
         for (int64_t i = t0; i < t0 + len; ++i) store_lp(lpp, lpd, i, pp[i]);
     }
   }
+}
+
+// Split-master Adam on the host: lo (int16 residuals), m, v (fp32), g (bf16/fp32), hi_in (bf16 weights staged from the
+// device), hi_out (bf16, may be the same buffer as g or hi_in).
+void cpu_adam_update_split(torch::Tensor lo, torch::Tensor m, torch::Tensor v, torch::Tensor g, torch::Tensor hi_in,
+                           torch::Tensor hi_out, int64_t step, double lr, double b1, double b2, double eps, double wd,
+                           bool bias_correction, bool adamw, double grad_scale) {
+  check_host(lo, "lo"); check_host(m, "m"); check_host(v, "v"); check_host(g, "g");
+  check_host(hi_in, "hi_in"); check_host(hi_out, "hi_out");
+  const int64_t n = lo.numel();
+  TORCH_CHECK(lo.scalar_type() == at::kShort && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat &&
+              hi_in.scalar_type() == at::kBFloat16 && hi_out.scalar_type() == at::kBFloat16,
+              "cpu_adam_split: lo int16, m/v fp32, hi bf16");
+  TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n && hi_in.numel() == n && hi_out.numel() == n,
+              "cpu_adam_split: size mismatch");
+  const int gd = dcode(g);
+  TORCH_CHECK(gd == 0 || gd == 1, "cpu_adam_split: grads must be fp32 or bf16");
+  const float bc1 = bias_correction ? 1.f - std::pow((float)b1, (float)step) : 1.f;
+  const float bc2 = bias_correction ? 1.f - std::pow((float)b2, (float)step) : 1.f;
+  const float step_size = 1.f / bc1, denom_scale = 1.f / std::sqrt(bc2);
+  int16_t* lp = lo.data_ptr<int16_t>();
+  float* mp = m.data_ptr<float>();
+  float* vp = v.data_ptr<float>();
+  const void* gp = g.data_ptr();
+  const uint16_t* hin = reinterpret_cast<const uint16_t*>(hi_in.data_ptr());
+  uint16_t* hout = reinterpret_cast<uint16_t*>(hi_out.data_ptr());
+#pragma omp parallel for schedule(static)
+  for (int64_t t0 = 0; t0 < n; t0 += TILE) {
+    const int64_t len = std::min(TILE, n - t0);
+    if (gd == 1)
+      adam_split_tile_bf16g(lp + t0, mp + t0, vp + t0, static_cast<const uint16_t*>(gp) + t0, hin + t0, hout + t0,
+                            len, lr, b1, b2, eps, wd, step_size, denom_scale, grad_scale, adamw);
+    else
+      adam_split_tile_f32g(lp + t0, mp + t0, vp + t0, static_cast<const float*>(gp) + t0, hin + t0, hout + t0, len,
+                           lr, b1, b2, eps, wd, step_size, denom_scale, grad_scale, adamw);
+  }
+}
+
+// dst (fp32) = src * alpha (first) or dst + src * alpha, src bf16 or fp32: host-side gradient accumulation
+void cpu_accumulate(torch::Tensor dst, torch::Tensor src, double alpha, bool first) {
+  check_host(dst, "dst"); check_host(src, "src");
+  const int64_t n = dst.numel();
+  TORCH_CHECK(dst.scalar_type() == at::kFloat && src.numel() == n, "cpu_accumulate: fp32 dst, same numel");
+  float* d = dst.data_ptr<float>();
+  const int sd = dcode(src);
+  const void* sp = src.data_ptr();
+#pragma omp parallel for schedule(static)
+  for (int64_t t0 = 0; t0 < n; t0 += TILE) {
+    const int64_t len = std::min(TILE, n - t0);
+    if (sd == 1) acc_tile_bf16(d + t0, static_cast<const uint16_t*>(sp) + t0, len, alpha, first);
+    else
+      for (int64_t i = t0; i < t0 + len; ++i) {
+        const float f = load_any(sp, sd, i) * (float)alpha;
+        d[i] = first ? f : d[i] + f;
+      }
+  }
+}
+
+double cpu_sumsq(torch::Tensor src) {
+  check_host(src, "src");
+  TORCH_CHECK(src.scalar_type() == at::kFloat, "cpu_sumsq: fp32 only");
+  const int64_t n = src.numel();
+  const float* s = src.data_ptr<float>();
+  double acc = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : acc)
+  for (int64_t t0 = 0; t0 < n; t0 += TILE) acc += sumsq_tile(s + t0, std::min(TILE, n - t0));
+  return acc;
 }
 
 void cpu_adagrad_update(torch::Tensor p, torch::Tensor s, torch::Tensor g, c10::optional<torch::Tensor> lp, double lr,
@@ -221,9 +348,15 @@ std::string simd_level() {
 }
 
 void register_cpu_optim(pybind11::module& m) {
-  m.def("cpu_adam_update", &cpu_adam_update);
-  m.def("cpu_adagrad_update", &cpu_adagrad_update);
-  m.def("cpu_lion_update", &cpu_lion_update);
-  m.def("cpu_to_bf16", &cpu_to_bf16);
+  // the update loops run without the interpreter lock: the Twin-Flow worker thread steps the host partition while
+  // the main thread launches the device optimizer and the next forward
+  using nogil = pybind11::call_guard<pybind11::gil_scoped_release>;
+  m.def("cpu_adam_update", &cpu_adam_update, nogil());
+  m.def("cpu_adam_update_split", &cpu_adam_update_split, nogil());
+  m.def("cpu_accumulate", &cpu_accumulate, nogil());
+  m.def("cpu_sumsq", &cpu_sumsq, nogil());
+  m.def("cpu_adagrad_update", &cpu_adagrad_update, nogil());
+  m.def("cpu_lion_update", &cpu_lion_update, nogil());
+  m.def("cpu_to_bf16", &cpu_to_bf16, nogil());
   m.def("simd_level", &simd_level);
 }

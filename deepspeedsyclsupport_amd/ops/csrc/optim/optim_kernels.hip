@@ -132,6 +132,67 @@ __global__ void __launch_bounds__(256) adam_mt_kernel(MTTable t, AdamArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------- split-master Adam (bf16 weight + 16 low bits)
+// The fp32 master value is not stored separately: its bit pattern is (hi << 16) + sext(lo), where `hi` is the bf16
+// model weight itself (the master rounded to nearest, ties away from zero) and `lo` a signed 16-bit residual in
+// fp32 ulps. The update reconstructs the exact fp32 master, applies Adam and writes both halves back, so training
+// is bit-identical to an fp32 master whose bf16 copy is rounded half-up — at 2 B/param less memory and traffic.
+__device__ __forceinline__ float split_join(uint16_t hi, int16_t lo) {
+  return __uint_as_float(((uint32_t)hi << 16) + (uint32_t)(int32_t)lo);
+}
+__device__ __forceinline__ void split_cut(float f, uint16_t& hi, int16_t& lo) {
+  const uint32_t u = __float_as_uint(f);
+  hi = (uint16_t)((u + 0x8000u) >> 16);
+  lo = (int16_t)(u & 0xffffu);
+}
+
+template <typename TG>
+__global__ void __launch_bounds__(256) adam_mt_split_kernel(MTTable t, AdamArgs a) {
+  const int ti = mt_find(t, blockIdx.x);
+  const int64_t chunk = blockIdx.x - t.block_start[ti];
+  int16_t* lo = (int16_t*)t.p[ti];
+  float* m = (float*)t.m[ti];
+  float* v = (float*)t.v[ti];
+  const TG* g = (const TG*)t.g[ti];
+  uint16_t* hi = (uint16_t*)t.lp[ti];
+  const int64_t n = t.n[ti];
+  const int64_t beg = chunk * MT_CHUNK, end = min(n, beg + (int64_t)MT_CHUNK);
+  const float step_size = 1.f / a.bias_correction1;
+  const float denom_scale = rsqrtf(a.bias_correction2);
+  if (t.vec_ok[ti]) {
+    for (int64_t o = beg + threadIdx.x * 8; o < end; o += 256 * 8) {
+      float pp[8], mm[8], vv[8], gg[8];
+      s16x8 h = *reinterpret_cast<const s16x8*>(hi + o);
+      s16x8 l = *reinterpret_cast<const s16x8*>(lo + o);
+      Vec8<float>::load(m + o, mm);
+      Vec8<float>::load(v + o, vv);
+      Vec8<TG>::load(g + o, gg);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pp[j] = split_join((uint16_t)h[j], (int16_t)l[j]);
+        adam_elem(pp[j], mm[j], vv[j], gg[j], a, step_size, denom_scale);
+        uint16_t hh; int16_t ll;
+        split_cut(pp[j], hh, ll);
+        h[j] = (short)hh;
+        l[j] = ll;
+      }
+      *reinterpret_cast<s16x8*>(hi + o) = h;
+      *reinterpret_cast<s16x8*>(lo + o) = l;
+      Vec8<float>::store(m + o, mm);
+      Vec8<float>::store(v + o, vv);
+    }
+  } else {
+    for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
+      float pp = split_join(hi[i], lo[i]), mm = m[i], vv = v[i];
+      adam_elem(pp, mm, vv, to_f32(g[i]), a, step_size, denom_scale);
+      uint16_t hh; int16_t ll;
+      split_cut(pp, hh, ll);
+      hi[i] = hh; lo[i] = ll; m[i] = mm; v[i] = vv;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- Lion
 struct LionArgs {
   float lr, beta1, beta2, weight_decay, grad_scale;
@@ -332,6 +393,31 @@ extern "C" int ds_adam_multi(void** p, void** m, void** v, const void** g, void*
     if (blocks == 0) continue;
     DISPATCH_P(p_dtype, DISPATCH_G(g_dtype, DISPATCH_LP(lp ? lp_dtype : -1,
         hipLaunchKernelGGL((adam_mt_kernel<TP, TG, TL, HL>), dim3(blocks), dim3(256), 0, stream, t, a))));
+    DS_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// Split-master multi-tensor Adam: lo (int16 residuals), m/v (fp32), g (any dtype), hi (bf16 weights, in/out).
+extern "C" int ds_adam_multi_split(void** lo, void** m, void** v, const void** g, void** hi, const int64_t* n,
+                                   int count, int g_dtype, float lr, float beta1, float beta2, float eps, float wd,
+                                   float bc1, float bc2, float grad_scale, int adamw_mode, hipStream_t stream) {
+  AdamArgs a{lr, beta1, beta2, eps, wd, bc1, bc2, grad_scale, adamw_mode};
+  for (int base = 0; base < count; base += MT_MAX) {
+    MTTable t;
+    t.count = count - base < MT_MAX ? count - base : MT_MAX;
+    int blocks = 0;
+    for (int i = 0; i < t.count; ++i) {
+      const int k = base + i;
+      t.p[i] = lo[k]; t.m[i] = m[k]; t.v[i] = v[k]; t.g[i] = g[k]; t.lp[i] = hi[k]; t.n[i] = n[k];
+      t.block_start[i] = blocks;
+      blocks += (int)((n[k] + MT_CHUNK - 1) / MT_CHUNK);
+      auto al = [](const void* q) { return ((uintptr_t)q % 16) == 0; };
+      t.vec_ok[i] = ((n[k] % 8 == 0) && al(lo[k]) && al(m[k]) && al(v[k]) && al(g[k]) && al(hi[k])) ? 1 : 0;
+    }
+    t.block_start[t.count] = blocks;
+    if (blocks == 0) continue;
+    DISPATCH_G(g_dtype, hipLaunchKernelGGL((adam_mt_split_kernel<TG>), dim3(blocks), dim3(256), 0, stream, t, a));
     DS_CHECK_LAUNCH();
   }
   return 0;

@@ -60,6 +60,9 @@ class FP16Config(DeepSpeedConfigModel):
 class BF16Config(DeepSpeedConfigModel):
     enabled: bool = False
     immediate_grad_update: bool = False
+    # MI355X addition: keep the fp32 master as (bf16 weight, 16-bit residual) instead of a separate fp32 copy:
+    # 2 B/param less optimizer state, bit-exact fp32 master arithmetic (weights rounded half away from zero)
+    split_master_weights: bool = False
 
 
 class AMPConfig(DeepSpeedConfigModel):

@@ -499,6 +499,8 @@ class DeepSpeedEngine(nn.Module):
             self._moq_quantize()
         if self.module.training and self.progressive_layer_drop is not None:
             kwargs.update(self.progressive_layer_drop.get_state())
+        if self.optimizer is not None:
+            self.optimizer.offload_pre_forward()
         loss = self.module(*inputs, **kwargs)
         self.timers(FORWARD_MICRO_TIMER).stop()
         return loss
@@ -629,6 +631,7 @@ class DeepSpeedEngine(nn.Module):
             sd = self.module_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
             return OrderedDict((k, v.detach().cpu().clone()) for k, v in sd.items())
         opt = self.optimizer
+        opt.join_offload()
         keep = (not rank0_only) or dist.get_rank() == 0
         names = {id(p): n for n, p in self.module.named_parameters()}
         out = OrderedDict()

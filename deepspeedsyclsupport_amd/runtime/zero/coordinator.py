@@ -172,11 +172,15 @@ class ParamCoordinator:
         if self.ag_stream is not None:
             self.ag_stream.wait_stream(compute)
             with self.acc.stream(self.ag_stream):
+                if opt.off is not None and g.pieces:
+                    opt.off.wait_group(g)  # host-stepped weights of this shard must have landed (orders ag_stream)
                 g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
                 self._gather(g)
                 g.ag_event = self.acc.Event()
                 g.ag_event.record(self.ag_stream)
         else:
+            if opt.off is not None and g.pieces:
+                opt.off.wait_group(g)
             g.full = torch.empty(g.padded, dtype=opt.dtype, device=opt.device)
             self._gather(g)
             g.ag_event = None

@@ -153,22 +153,24 @@ class FlatZeroOptimizer(ZeROOptimizer):
         self._global_grad_norm = None
         self.offload = False
         self.offload_ratio = 0.0
-        if self.zc is not None and self.zc.offload_optimizer is not None and \
-                str(self.zc.offload_optimizer.device.value if hasattr(self.zc.offload_optimizer.device, "value") else self.zc.offload_optimizer.device) in ("cpu", "nvme"):
+        self.offload_nvme = False
+        self.off = None  # OffloadedState: host / NVMe resident optimizer state and its transfer pipelines
+        oc = self.zc.offload_optimizer if self.zc is not None else None
+        if oc is not None and _devname(oc.device) in ("cpu", "nvme"):
             self.offload = True
-            self.offload_ratio = float(self.zc.offload_optimizer.ratio)
-            self.offload_pin = bool(self.zc.offload_optimizer.pin_memory)
+            self.offload_ratio = float(oc.ratio)
+            self.offload_pin = bool(oc.pin_memory)
+            self.offload_nvme = _devname(oc.device) == "nvme"
         self.nvme_swapper = None
-        if self.offload and str(getattr(self.zc.offload_optimizer.device, "value",
-                                        self.zc.offload_optimizer.device)) == "nvme":
-            from ..swap_tensor import OptimizerStateSwapper
-            path = self.zc.offload_optimizer.nvme_path or "/tmp/ds_nvme_swap"
-            folder = os.path.join(path, f"zero_stage_{self.stage}", "optimizer", f"rank{dist.get_rank()}")
-            # ZeRO-Infinity: the fp32 master AND the moments of the host partition live on NVMe, streamed in
-            # sub_group_size chunks (reference partitioned_optimizer_swapper: fp32 params + optimizer states)
-            chunk = int(min(getattr(self.zc, "sub_group_size", 64 * 2**20) or 64 * 2**20, 64 * 2**20))
-            self.nvme_swapper = OptimizerStateSwapper(ds_config.aio_config, folder, chunk_numel=max(chunk, 1),
-                                                      pin=self.device.type == "cuda", with_master=True)
+        # split masters (bf16.split_master_weights): master bits = (bf16 weight << 16) + int16 residual
+        self.split_master = bool(getattr(getattr(ds_config, "bf16_config", None), "split_master_weights", False))
+        if self.split_master and dtype != torch.bfloat16:
+            raise ValueError("bf16.split_master_weights needs bf16 training")
+        # gradient scaling around the reduction (reference `runtime/engine.py:2331-2341`, passed to ZeRO at
+        # `engine.py:1523,1595,1636`): prescale divides by the data-parallel size before the collective, otherwise
+        # gradient_predivide_factor is applied before it and the remainder after
+        self.prescale_gradients = bool(getattr(ds_config, "prescale_gradients", False))
+        self.predivide = float(getattr(ds_config, "gradient_predivide_factor", 1.0) or 1.0)
         # ZeRO-Infinity parameter offload: non-persistent ZeRO-3 shards live in pinned host memory (cpu) or in
         # per-group files on NVMe mapped into the address space (nvme); every fetch streams them H2D on the
         # all-gather stream ahead of use (trace-driven prefetch), so HBM only holds the live working set.
@@ -356,7 +358,11 @@ class FlatZeroOptimizer(ZeROOptimizer):
 
     @torch.no_grad()
     def _build_master(self):
-        """fp32 master buffers per optimizer group, as concatenated runs (rank-segment ∩ optimizer group)."""
+        """Optimizer-state layout: per optimizer group the local elements are concatenated "runs" (rank-segment ∩
+        optimizer group). The LAST `ratio` of each group's elements (in forward order) is offloaded — those layers'
+        gradients are final first in backward, so their copies down overlap the rest of backward, and their weights
+        are needed last by the next forward, so the host update overlaps it — and handed to `OffloadedState`; the
+        rest keeps fp32 master (or int16 residuals with split masters) and moments on the device."""
         og_len = [0] * self.num_og
         run_specs = []
         for g in self.groups:
@@ -371,15 +377,23 @@ class FlatZeroOptimizer(ZeROOptimizer):
             for s, e, og in runs:
                 run_specs.append((g, s, e, og))
                 og_len[og] += e - s
-        # Twin-Flow split: the first `ratio` of each og's elements live (and are stepped) on the host
-        host_budget = [int(l * self.offload_ratio) if self.offload else 0 for l in og_len]
-        self.master, self.master_host = [], []
-        self.grad_acc, self.grad_acc_host = [], []
+        if self.split_master and not self._fused_adam:
+            raise ValueError("bf16.split_master_weights is implemented for Adam / AdamW only")
+        boundary = [l - int(l * self.offload_ratio) if self.offload else l for l in og_len]
+        pos = [0] * self.num_og
         dev_len = [0] * self.num_og
         host_len = [0] * self.num_og
+        split_specs = []
         for g, s, e, og in run_specs:
+            # a run straddling the device/host boundary is cut there (at a 64-element multiple of its start)
+            cut = s + (boundary[og] - pos[og]) // ALIGN * ALIGN
+            pos[og] += e - s
+            if self.offload and s < cut < e:
+                split_specs += [(g, s, cut, og, False), (g, cut, e, og, True)]
+            else:
+                split_specs.append((g, s, e, og, self.offload and cut <= s))
+        for g, s, e, og, on_host in split_specs:
             n = e - s
-            on_host = host_len[og] + n <= host_budget[og] and self.offload
             if on_host:
                 moff = host_len[og]
                 host_len[og] += n
@@ -387,43 +401,93 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 moff = dev_len[og]
                 dev_len[og] += n
             g.runs.append((s - g.seg_lo, e - g.seg_lo, og, moff, on_host))
-        pin = self.device.type == "cuda" and self.offload and getattr(self, "offload_pin", True)
-        host_runs = [[] for _ in range(self.num_og)]
+        self.master = []
+        self.grad_acc = []
+        mdt = torch.int16 if self.split_master else torch.float32
+        for og in range(self.num_og):
+            self.master.append(torch.zeros(dev_len[og], dtype=mdt, device=self.device))
+            self.grad_acc.append(None)  # fp32 accumulator, allocated only when a path needs it
+        for g in self.groups:
+            g.pieces = []    # offloaded runs of this group (OffloadedState pieces)
+            g.host_map = {}
+            for (s, e, og, moff, on_host) in g.runs:
+                if not on_host and not self.split_master:
+                    self.master[og][moff:moff + e - s].copy_(g.shard[s:e])
+        if self.offload and any(host_len):
+            self._build_offload(host_len)
+        # hand the optimizer one flat parameter per group (its param_groups / lr schedule stay authoritative); with
+        # split masters there is no fp32 tensor to hand over, an empty placeholder keys the moments instead
+        self.fp32_flat = []
+        for og, group in enumerate(self.optimizer.param_groups):
+            data = torch.empty(0, dtype=torch.float32, device=self.device) if self.split_master else self.master[og]
+            mp = nn.Parameter(data, requires_grad=False)
+            self.fp32_flat.append(mp)
+            group["params"] = [mp]
+
+    def _build_offload(self, host_len):
+        from .offload import OffloadedState
+        oc = self.zc.offload_optimizer
+        pin = self.device.type == "cuda" and getattr(self, "offload_pin", True)
+        resident = list(host_len)
+        if self.offload_nvme:
+            budget = int(getattr(oc, "max_in_cpu", 0) or 0)
+            for og in range(self.num_og):
+                resident[og] = min(host_len[og], budget)
+                budget -= resident[og]
+            from ..swap_tensor import OptimizerStateSwapper
+            path = oc.nvme_path or "/tmp/ds_nvme_swap"
+            folder = os.path.join(path, f"zero_stage_{self.stage}", "optimizer", f"rank{dist.get_rank()}")
+            # ZeRO-Infinity: master AND moments of the NVMe tail live in files, streamed in sub_group_size chunks
+            # (reference partitioned_optimizer_swapper: fp32 params + optimizer states)
+            chunk = int(min(getattr(self.zc, "sub_group_size", 64 * 2**20) or 64 * 2**20, 64 * 2**20))
+            self.nvme_swapper = OptimizerStateSwapper(self.cfg.aio_config, folder, chunk_numel=max(chunk, 1),
+                                                      pin=self.device.type == "cuda", with_master=True,
+                                                      master_dtype=torch.int16 if self.split_master
+                                                      else torch.float32)
+        self.off = OffloadedState(self, host_len, resident, self.split_master, pin, self.nvme_swapper,
+                                  overlap_forward=bool(getattr(oc, "overlap_forward", False)))
         for g in self.groups:
             for (s, e, og, moff, on_host) in g.runs:
                 if on_host:
-                    host_runs[og].append((moff, e - s, g, s))
+                    g.pieces.append(self.off.add_piece(og, moff, e - s, g, s))
+        self.off.finalize()
+        for p in self.off.all_pieces:
+            self.off.init_master(p)
         for og in range(self.num_og):
-            self.master.append(torch.zeros(dev_len[og], dtype=torch.float32, device=self.device))
-            self.grad_acc.append(None)  # fp32 accumulator, allocated only when a path needs it
-            if host_len[og] and self.nvme_swapper is not None:
-                from ..swap_tensor.optimizer_swapper import NvmeFlat
-
-                def init(lo, hi, buf, runs=host_runs[og]):  # fill one chunk of the master from the shards
-                    buf.zero_()
-                    for moff, n, g, s in runs:
-                        a, b = max(lo, moff), min(hi, moff + n)
-                        if a < b:
-                            buf[a - lo:b - lo].copy_(g.shard[s + a - moff:s + b - moff])
-
-                self.nvme_swapper.register(og, host_len[og], master_init=init)
-                self.master_host.append(NvmeFlat(self.nvme_swapper, og, host_len[og]))
-            else:
-                self.master_host.append(_host_zeros(host_len[og], torch.float32, pin) if host_len[og] else None)
-            self.grad_acc_host.append(_host_zeros(host_len[og], torch.float32, pin) if host_len[og] else None)
+            if host_len[og] > resident[og]:
+                self.nvme_swapper.register(og, host_len[og] - resident[og], master_init=self.off.nvme_master_init(og))
+        # LOCAL-mode staging map: param index -> [(piece, offset in piece, offset in param, numel)]
         for g in self.groups:
-            for (s, e, og, moff, on_host) in g.runs:
-                if on_host and self.nvme_swapper is not None:
-                    continue  # written into the NVMe master above
-                dst = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
-                dst.copy_(g.shard[s:e])
-        # hand the fp32 buffers to the wrapped optimizer (its param_groups / lr schedule stay authoritative)
-        self.fp32_flat = []
-        for og, group in enumerate(self.optimizer.param_groups):
-            mp = nn.Parameter(self.master[og], requires_grad=False)
-            self.fp32_flat.append(mp)
-            group["params"] = [mp]
-        self.host_states = {}  # og -> [exp_avg, exp_avg_sq, step] for the Twin-Flow host part
+            g.host_map = {}
+            for piece in g.pieces:
+                lo, hi = g.seg_lo + piece.s, g.seg_lo + piece.s + piece.n
+                for i in range(len(g.params)):
+                    a, n = g.offsets[i], g.numels[i]
+                    x0, x1 = max(a, lo), min(a + n, hi)
+                    if x0 < x1:
+                        g.host_map.setdefault(i, []).append((piece, x0 - lo, x0 - a, x1 - x0))
+        if self.off.overlap_forward:
+            self._install_offload_waits()
+
+    def _install_offload_waits(self):
+        """overlap_forward: each module owning offloaded weights waits for its own copy before its forward."""
+        self._offload_wait_hooks = []
+        for g in self.groups:
+            if g.pieces and g.module is not None and g.persistent:  # fetched groups wait inside the coordinator
+                self._offload_wait_hooks.append(
+                    g.module.register_forward_pre_hook(lambda m, a, g=g: self.off.wait_group(g)))
+
+    def offload_pre_forward(self):
+        """Engine hook at the start of forward: groups without an owning module wait here (overlap_forward)."""
+        if self.off is not None and self.off.overlap_forward:
+            for g in self.groups:
+                if g.pieces and g.module is None and g.persistent:
+                    self.off.wait_group(g)
+
+    def join_offload(self):
+        """Block until the host partition's step has finished and its weights are back in the shards."""
+        if self.off is not None:
+            self.off.wait()
 
     def _ensure_grad_acc(self, og):
         if self.grad_acc[og] is None:
@@ -457,7 +521,7 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 self._point_grads(g)
         for p in self.opt_params:
             g, _ = self.param_group[id(p)]
-            if g.mode != self.LOCAL or self.coordinator_needed():
+            if g.mode != self.LOCAL or self.coordinator_needed() or g.pieces:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_ready_hook))
 
     def coordinator_needed(self):
@@ -474,6 +538,8 @@ class FlatZeroOptimizer(ZeROOptimizer):
 
     def _grad_ready_hook(self, p):
         g, i = self.param_group[id(p)]
+        if p.grad is not None and p.grad.is_sparse:
+            p.grad = p.grad.to_dense()  # nn.Embedding(sparse=True): the flat buffers and the fused Adam are dense
         if g.mode == self.PRESET:
             view = g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]]
             if p.grad is None or p.grad.data_ptr() != view.data_ptr():
@@ -486,6 +552,13 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
             g.grad_flat[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1))
             p.grad = None
+        elif g.pieces and self.is_gradient_accumulation_boundary and i in g.host_map:
+            # LOCAL + offload: this parameter's (accumulated) gradient is final; send it down and free it
+            flat = p.grad.reshape(-1)
+            for (piece, poff, lo, n) in g.host_map[i]:
+                self.off.stage_grad(piece, flat[lo:lo + n], 1.0 / self._div(g), off=poff)
+            if sum(n for (_, _, _, n) in g.host_map[i]) == g.numels[i]:
+                p.grad = None  # (a parameter cut by the device/host boundary keeps its gradient for the device part)
         if self.safe_mode and g.pending <= 0:
             from .utils import ZeRORuntimeException
             raise ZeRORuntimeException(f"fetch group {g.idx}: more gradients than parameters in one backward pass "
@@ -514,8 +587,16 @@ class FlatZeroOptimizer(ZeROOptimizer):
             return float(g.reduce_dp)
         return float(self.dp)
 
-    def _prescale(self, g=None):
-        return self.comm_dtype == torch.float16 and self._div(g) > 1
+    def _pre_factor(self, g=None):
+        """Factor applied to the gradients BEFORE the collective (the rest of 1/div is applied after it, folded into
+        the optimizer's gradient scale): 1/div with prescale_gradients (or fp16 communication, where the sum could
+        overflow), else 1/gradient_predivide_factor."""
+        div = self._div(g)
+        if div <= 1:
+            return 1.0
+        if self.prescale_gradients or self.comm_dtype == torch.float16:
+            return 1.0 / div
+        return 1.0 / self.predivide if self.predivide != 1.0 else 1.0
 
     @instrument_w_nvtx
     def _reduce_group(self, g):
@@ -533,8 +614,9 @@ class FlatZeroOptimizer(ZeROOptimizer):
             self.rs_stream.wait_stream(compute)
         with ctx:
             comm = src if src.dtype == self.comm_dtype else src.to(self.comm_dtype)
-            if self._prescale(g):
-                comm.mul_(1.0 / self._div(g))
+            pre = self._pre_factor(g)
+            if pre != 1.0:
+                comm.mul_(pre)
             if self._local_grads():
                 out = comm  # a communication-compressed optimizer (1-bit Adam/LAMB, 0/1 Adam) averages on its own
             elif g.partition:
@@ -549,9 +631,12 @@ class FlatZeroOptimizer(ZeROOptimizer):
             else:
                 dist.all_reduce(comm, group=g.dp_group)
                 out = comm[g.seg_lo:g.seg_lo + g.seg]
-            if g.mode == self.COPY and self.gas > 1:
+            accumulate = g.mode == self.COPY and self.gas > 1
+            for piece in g.pieces:  # offloaded runs: the reduced segment goes down to the host now
+                self.off.stage_grad(piece, out[piece.s:piece.s + piece.n], self._alpha(g), accumulate=accumulate)
+            if accumulate:
                 self._accumulate_runs(g, out, self._alpha(g))
-            else:
+            elif any(not r[4] for r in g.runs):
                 g.red_out = out
             if g.mode == self.COPY:
                 if self.rs_stream is not None:
@@ -559,25 +644,21 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 g.grad_flat = None
 
     def _alpha(self, g=None):
-        return 1.0 if (self._prescale(g) or self._div(g) == 1) else 1.0 / self._div(g)
+        """Factor still owed to the reduced gradient: 1 / (div * pre_factor)."""
+        div = self._div(g)
+        return 1.0 if div == 1 else 1.0 / (div * self._pre_factor(g))
 
     def _accumulate_runs(self, g, seg_grad, alpha):
         first = not g._acc_valid
         for (s, e, og, moff, on_host) in g.runs:
-            src = seg_grad[s:e]
             if on_host:
-                dst = self.grad_acc_host[og][moff:moff + e - s]
-                tmp = src.float().mul_(alpha).cpu()
-                if first:
-                    dst.copy_(tmp)
-                else:
-                    dst.add_(tmp)
+                continue  # accumulated on the host by OffloadedState
+            src = seg_grad[s:e]
+            dst = self._ensure_grad_acc(og)[moff:moff + e - s]
+            if first:
+                torch.mul(src, alpha, out=dst) if alpha != 1.0 else dst.copy_(src)
             else:
-                dst = self._ensure_grad_acc(og)[moff:moff + e - s]
-                if first:
-                    torch.mul(src, alpha, out=dst) if alpha != 1.0 else dst.copy_(src)
-                else:
-                    dst.add_(src, alpha=alpha)
+                dst.add_(src, alpha=alpha)
         g._acc_valid = True
 
     def backward_prologue(self):
@@ -665,33 +746,38 @@ class FlatZeroOptimizer(ZeROOptimizer):
         self.mics_replicas = self.dp // S
 
     def _grad_items(self):
-        """[(og, moff, n, grad_1d, lp_1d, scale, on_host)] covering every local master element that has a gradient."""
+        """[(og, moff, n, grad_1d, lp_1d, scale)] covering every DEVICE-resident master element that has a gradient
+        (offloaded elements were staged to the host during backward)."""
         items = []
         for g in self.groups:
             alpha, div = self._alpha(g), self._div(g)
             for (s, e, og, moff, on_host) in g.runs:
+                if on_host:
+                    continue
                 if g.mode == self.LOCAL:
                     for i, p in enumerate(g.params):
                         a, n = g.offsets[i], g.numels[i]
                         lo, hi = max(a, g.seg_lo + s), min(a + n, g.seg_lo + e)
                         if lo >= hi or p.grad is None:
                             continue
+                        if p.grad.is_sparse:
+                            p.grad = p.grad.to_dense()
                         gr = p.grad.reshape(-1)[lo - a:hi - a]
                         items.append((og, moff + lo - g.seg_lo - s, hi - lo, gr, g.shard[lo - g.seg_lo:hi - g.seg_lo],
-                                      1.0 / div, on_host))
+                                      1.0 / div))
                 elif g._acc_valid:
-                    src = (self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s]
-                    items.append((og, moff, e - s, src, g.shard[s:e], 1.0, on_host))
+                    items.append((og, moff, e - s, self.grad_acc[og][moff:moff + e - s], g.shard[s:e], 1.0))
                 elif g.red_out is not None:
-                    items.append((og, moff, e - s, g.red_out[s:e], g.shard[s:e], alpha, on_host))
+                    items.append((og, moff, e - s, g.red_out[s:e], g.shard[s:e], alpha))
         return items
 
     @torch.no_grad()
     def _global_norm_sq(self, items):
         """Squared global grad norm: each rank sums its unique elements (replicas divided out) and ONE all-reduce over
-        the world adds dense DP partitions, expert partitions and tensor-parallel shards alike."""
+        the world adds dense DP partitions, expert partitions and tensor-parallel shards alike. Gradients already
+        staged to the host contribute the sums taken on their way down."""
         classes = defaultdict(list)
-        for (og, moff, n, gr, lp, scale, on_host) in items:
+        for (og, moff, n, gr, lp, scale) in items:
             classes[(og, scale, gr.device.type)].append(gr)
         sq = torch.zeros((), dtype=torch.float32, device=self.device)
         for (og, scale, devtype), ts in classes.items():
@@ -700,6 +786,10 @@ class FlatZeroOptimizer(ZeROOptimizer):
             else:
                 s = sum((t.float().pow(2).sum() for t in ts), torch.zeros(())).to(self.device)
             sq = sq + s * (scale * scale) / self._og_replicas(og)
+        if self.off is not None:
+            for og, s in self.off.staged_norm_sq().items():
+                s = s.to(self.device) if torch.is_tensor(s) else torch.tensor(float(s), device=self.device)
+                sq = sq + s.float() / self._og_replicas(og)
         if self.world > 1:
             dist.all_reduce(sq)
         return sq
@@ -720,36 +810,44 @@ class FlatZeroOptimizer(ZeROOptimizer):
         if overflow:
             log_dist(f"Overflow detected. Skipping step. Attempted loss scale: {1 / scale}, reducing to "
                      f"{self.loss_scaler.loss_scale}", ranks=[0])
+            if self.off is not None:
+                self.off.discard()
             self._zero_grad_buffers()
             return
         clip = 1.0
         if self.clip_grad and self.clip_grad > 0 and norm_f > self.clip_grad:
             clip = self.clip_grad / (norm_f + 1e-6)
         grad_scale = scale * clip
-        host_items = [it for it in items if it[6]]
-        host_thread = None
-        if host_items:
-            self._stage_host_grads(host_items)
-            import threading
-            host_thread = threading.Thread(target=self._host_step, args=(grad_scale, ))
-            host_thread.start()
-        self._device_step([it for it in items if not it[6]], grad_scale)
-        if host_thread is not None:
-            host_thread.join()
-            self._host_writeback()
+        if self.off is not None:
+            # Twin-Flow: the host partition is stepped by the offload worker (CPU Adam + weight copies on the h2d
+            # stream) while this thread launches the device optimizer
+            self.off.step(grad_scale, self._host_hyper())
+        self._device_step(items, grad_scale)
+        if self.off is not None and (not self.off.overlap_forward or
+                                     any(g.partition and g.persistent and g.pieces for g in self.groups)):
+            self.off.wait()  # (persistent partitioned groups re-gather their shards right below)
         self._post_step_gather()
         self._zero_grad_buffers()
         self.global_steps += 1
 
-    def _stage_host_grads(self, host_items):
-        for (og, moff, n, gr, lp, s, on_host) in host_items:
-            if gr.device.type == "cpu" and gr.data_ptr() == self.grad_acc_host[og][moff:moff + n].data_ptr():
-                if s != 1.0:
-                    gr.mul_(s)
-                continue
-            self.grad_acc_host[og][moff:moff + n].copy_((gr.float() * s), non_blocking=True)
-        if self.device.type == "cuda":
-            torch.cuda.current_stream().synchronize()
+    def _host_hyper(self):
+        if not self._fused_adam:
+            raise NotImplementedError("optimizer offload steps the host partition with the native CPU Adam: use "
+                                      "Adam / AdamW (got " + type(self.optimizer).__name__ + ")")
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+        return [dict(lr=g["lr"], betas=tuple(g["betas"]), eps=g["eps"], weight_decay=g["weight_decay"],
+                     bias_correction=g.get("bias_correction", True), adamw=adamw)
+                for g in self.optimizer.param_groups]
+
+    def _moments(self, og):
+        """Device-resident Adam state of og (created on first use), keyed by the group's flat parameter."""
+        st = self.optimizer.state[self.fp32_flat[og]]
+        if len(st) == 0:
+            n = self.master[og].numel()
+            st["step"] = 0
+            st["exp_avg"] = torch.zeros(n, dtype=torch.float32, device=self.device)
+            st["exp_avg_sq"] = torch.zeros(n, dtype=torch.float32, device=self.device)
+        return st
 
     @instrument_w_nvtx
     def _device_step(self, items, grad_scale):
@@ -759,14 +857,10 @@ class FlatZeroOptimizer(ZeROOptimizer):
             for it in items:
                 by_og[it[0]].append(it)
             for og, group in enumerate(self.optimizer.param_groups):
-                fp = self.fp32_flat[og]
-                st = self.optimizer.state[fp]
-                if len(st) == 0:
-                    st["step"] = 0
-                    st["exp_avg"] = torch.zeros_like(fp.data)
-                    st["exp_avg_sq"] = torch.zeros_like(fp.data)
+                master = self.master[og]
+                st = self._moments(og)
                 st["step"] += 1
-                if fp.numel() == 0 or not by_og.get(og):
+                if master.numel() == 0 or not by_og.get(og):
                     continue
                 b1, b2 = group["betas"]
                 step = st["step"]
@@ -775,91 +869,58 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 bc2 = 1 - b2**step if bc else 1.0
                 # one multi-tensor launch per (grad dtype, grad scale) class
                 classes = defaultdict(list)
-                for (_, moff, n, gr, lp, s, _h) in by_og[og]:
+                for (_, moff, n, gr, lp, s) in by_og[og]:
                     classes[(gr.dtype, s)].append((moff, n, gr, lp))
                 for (gdt, s), lst in classes.items():
-                    ps = [fp.data[moff:moff + n] for moff, n, _, _ in lst]
+                    ps = [master[moff:moff + n] for moff, n, _, _ in lst]
                     ms = [st["exp_avg"][moff:moff + n] for moff, n, _, _ in lst]
                     vs = [st["exp_avg_sq"][moff:moff + n] for moff, n, _, _ in lst]
                     gs = [gr for _, _, gr, _ in lst]
                     lps = [lp for _, _, _, lp in lst]
-                    if fp.is_cuda:
-                        # offloaded shards: the kernel writes a device copy, streamed back to the host home after
+                    if master.is_cuda:
+                        # offloaded shards: the kernel works on a device copy, streamed back to the host home after
                         back = [(i, lp) for i, lp in enumerate(lps) if not lp.is_cuda]
                         for i, lp in back:
-                            lps[i] = torch.empty(lp.numel(), dtype=lp.dtype, device=fp.device)
-                        native.hip_ops().adam_multi(ps, ms, vs, gs, lps, group["lr"], b1, b2, group["eps"],
-                                                    group["weight_decay"], bc1, bc2, grad_scale * s, adamw)
+                            lps[i] = lp.to(master.device, non_blocking=True) if self.split_master else \
+                                torch.empty(lp.numel(), dtype=lp.dtype, device=master.device)
+                        if self.split_master:
+                            native.hip_ops().adam_multi_split(ps, ms, vs, gs, lps, group["lr"], b1, b2, group["eps"],
+                                                              group["weight_decay"], bc1, bc2, grad_scale * s, adamw)
+                        else:
+                            native.hip_ops().adam_multi(ps, ms, vs, gs, lps, group["lr"], b1, b2, group["eps"],
+                                                        group["weight_decay"], bc1, bc2, grad_scale * s, adamw)
                         for i, lp in back:
                             lp.copy_(lps[i], non_blocking=lp.is_pinned())
                     else:
                         # host flats (CPU accelerator / gloo): the native AVX-512 Adam (csrc/cpu/cpu_optim.cpp)
                         cpu = native.cpu_ops()
                         for p_, m_, v_, g_, lp_ in zip(ps, ms, vs, gs, lps):
-                            cpu.cpu_adam_update(p_, m_, v_, g_.contiguous(), lp_, step, group["lr"], b1, b2,
-                                                group["eps"], group["weight_decay"], bc, adamw, grad_scale * s)
+                            if self.split_master:
+                                hi = lp_.contiguous()
+                                cpu.cpu_adam_update_split(p_, m_, v_, g_.contiguous(), hi, hi, step, group["lr"], b1,
+                                                          b2, group["eps"], group["weight_decay"], bc, adamw,
+                                                          grad_scale * s)
+                                if hi.data_ptr() != lp_.data_ptr():
+                                    lp_.copy_(hi)
+                            else:
+                                cpu.cpu_adam_update(p_, m_, v_, g_.contiguous(), lp_, step, group["lr"], b1, b2,
+                                                    group["eps"], group["weight_decay"], bc, adamw, grad_scale * s)
         else:
             # generic torch optimizer over the fp32 flats: materialise scaled fp32 grads, step, copy to shards
             for og in range(self.num_og):
                 self._ensure_grad_acc(og)
-            touched = set()
-            for (og, moff, n, gr, lp, s, _h) in items:
+            for (og, moff, n, gr, lp, s) in items:
                 dst = self.grad_acc[og][moff:moff + n]
                 if dst.data_ptr() == gr.data_ptr():
                     dst.mul_(grad_scale)
                 else:
                     torch.mul(gr, grad_scale * s, out=dst) if gr.dtype == torch.float32 else \
                         dst.copy_(gr).mul_(grad_scale * s)
-                touched.add(og)
             for og in range(self.num_og):
                 self.fp32_flat[og].grad = self.grad_acc[og]
             self.optimizer.step()
-            for (og, moff, n, gr, lp, s, _h) in items:
+            for (og, moff, n, gr, lp, s) in items:
                 lp.copy_(self.master[og][moff:moff + n])
-
-    @instrument_w_nvtx
-    def _host_step(self, grad_scale):
-        """Twin-Flow host half: native CPU Adam on pinned fp32 partitions (runs on a worker thread, concurrently
-        with the device Adam launched on the main thread)."""
-        from ...ops.native import cpu_ops
-        if not hasattr(self, "_host_lp"):
-            self._host_lp = {}
-        for og, group in enumerate(self.optimizer.param_groups):
-            hp = self.master_host[og]
-            if hp is None:
-                continue
-            b1, b2 = group["betas"]
-            lp = self._host_lp.get(og)
-            if lp is None:
-                lp = _host_zeros(hp.numel(), self.dtype, self.device.type == "cuda")
-                self._host_lp[og] = lp
-            adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
-            bc = group.get("bias_correction", True)
-            gr = self.grad_acc_host[og]
-            if self.nvme_swapper is not None:
-                # ZeRO-Infinity: master + moments stream from NVMe chunk by chunk (read-ahead / write-behind)
-                if og not in self.nvme_swapper.sizes:
-                    self.nvme_swapper.register(og, hp.numel())
-
-                def upd(lo, hi, m, v, step, master, lp=lp, gr=gr, group=group, b1=b1, b2=b2):
-                    cpu_ops().cpu_adam_update(master, m, v, gr[lo:hi], lp[lo:hi], step, group["lr"], b1, b2,
-                                              group["eps"], group["weight_decay"], bc, adamw, grad_scale)
-
-                self.nvme_swapper.step(og, upd)
-                continue
-            st = self.host_states.get(og)
-            if st is None:
-                st = [torch.zeros_like(hp), torch.zeros_like(hp), 0]
-                self.host_states[og] = st
-            st[2] += 1
-            cpu_ops().cpu_adam_update(hp, st[0], st[1], gr, lp, st[2], group["lr"], b1, b2, group["eps"],
-                                      group["weight_decay"], bc, adamw, grad_scale)
-
-    def _host_writeback(self):
-        for g in self.groups:
-            for (s, e, og, moff, on_host) in g.runs:
-                if on_host:
-                    g.shard[s:e].copy_(self._host_lp[og][moff:moff + e - s], non_blocking=True)
 
     def _post_step_gather(self):
         """Refresh full params of persistent groups from the updated shards (ZeRO-1/2, ZeRO-3 persistent)."""
@@ -906,30 +967,56 @@ class FlatZeroOptimizer(ZeROOptimizer):
         return loss * self.loss_scaler.loss_scale if self.dtype == torch.float16 else loss
 
     # ---------------------------------------------------------------- per-parameter views of flat fp32 state
-    _STATE_IDX = {"exp_avg": 0, "exp_avg_sq": 1}
+    # Two primitives address optimizer state by (group, run, segment range): `_run_read` returns fp32 values on the
+    # compute device, `_run_write` stores them. `key` is "fp32" (master), "exp_avg" or "exp_avg_sq". They hide where
+    # the state lives (device flat, host DRAM, NVMe) and how the master is stored (fp32, or bf16 weight + residual).
+    def _run_read(self, g, run, key, a, b):
+        s, e, og, moff, on_host = run
+        lo = moff + a - s
+        if on_host:
+            if key == "fp32" and self.split_master:
+                res = self.off.read_state(og, "residual", lo, lo + b - a).to(self.device)
+                return _split_join(g.shard[a:b].to(self.device), res)
+            t = self.off.read_state(og, key, lo, lo + b - a)
+            return None if t is None else t.to(self.device, torch.float32)
+        if key == "fp32":
+            m = self.master[og][lo:lo + b - a]
+            return _split_join(g.shard[a:b].to(self.device), m) if self.split_master else m
+        st = self.optimizer.state.get(self.fp32_flat[og], {})
+        t = st.get(key)
+        return None if t is None else t[lo:lo + b - a]
 
-    def _state_src(self, key):
-        """fetch(og, on_host) -> flat fp32 tensor holding `key` ('fp32' master or an optimizer state) for og."""
-        def fetch(og, on_host):
-            if key == "fp32":
-                return (self.master_host if on_host else self.master)[og]
+    def _run_write(self, g, run, key, a, values, also_shard=False):
+        s, e, og, moff, on_host = run
+        lo = moff + a - s
+        n = values.numel()
+        values = values.reshape(-1).to(torch.float32)
+        if key == "fp32" and self.split_master:
+            hi, res = _split_cut(values.to(self.device))
+            g.shard[a:a + n].copy_(hi)  # the weight IS the upper half of the master
             if on_host:
-                if self.nvme_swapper is not None and og in self.nvme_swapper.sizes:
-                    return self.nvme_swapper.read_full(og)[self._STATE_IDX[key]]
-                st = self.host_states.get(og)
-                return None if st is None else st[self._STATE_IDX[key]]
-            st = self.optimizer.state.get(self.fp32_flat[og], {})
-            return st.get(key)
-        return fetch
+                self.off.write_state(og, "residual", lo, res)
+            else:
+                self.master[og][lo:lo + n].copy_(res)
+            return
+        if on_host:
+            self.off.write_state(og, key, lo, values)
+        elif key == "fp32":
+            self.master[og][lo:lo + n].copy_(values)
+        else:
+            self._moments(og)[key][lo:lo + n].copy_(values)
+        if key == "fp32" and also_shard:
+            g.shard[a:a + n].copy_(values)
 
     @torch.no_grad()
-    def _gather_param(self, p, fetch):
+    def _gather_param(self, p, key):
+        self.join_offload()
         g, i = self.param_group[id(p)]
         seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
-        for (s, e, og, moff, on_host) in g.runs:
-            src = fetch(og, on_host)
+        for run in g.runs:
+            src = self._run_read(g, run, key, run[0], run[1])
             if src is not None:
-                seg32[s:e].copy_(src[moff:moff + e - s])
+                seg32[run[0]:run[1]].copy_(src)
         if g.partition:
             full = torch.empty(g.padded, dtype=torch.float32, device=self.device)
             dist.all_gather_into_tensor(full, seg32, group=g.dp_group)
@@ -938,76 +1025,68 @@ class FlatZeroOptimizer(ZeROOptimizer):
         return full[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).clone()
 
     @torch.no_grad()
-    def _scatter_param(self, p, value, fetch, also_shard=False):
+    def _scatter_param(self, p, value, key, also_shard=False):
+        self.join_offload()
         g, i = self.param_group[id(p)]
         flat = value.reshape(-1).to(torch.float32)
         a = g.offsets[i]
-        for (s, e, og, moff, on_host) in g.runs:
-            lo, hi = g.seg_lo + s, g.seg_lo + e
+        for run in g.runs:
+            lo, hi = g.seg_lo + run[0], g.seg_lo + run[1]
             x0, x1 = max(lo, a), min(hi, a + g.numels[i])
             if x0 < x1:
-                dst = fetch(og, on_host)
-                if dst is not None:
-                    _flat_write(dst, moff + x0 - lo, flat[x0 - a:x1 - a])
-                if also_shard:
-                    g.shard[x0 - g.seg_lo:x1 - g.seg_lo].copy_(flat[x0 - a:x1 - a])
+                self._run_write(g, run, key, x0 - g.seg_lo, flat[x0 - a:x1 - a], also_shard=also_shard)
 
-    def _local_fragment(self, p, fetch):
+    def _local_fragment(self, p, key):
         """Elements of `p` owned by this rank's partition (flat fp32), or None."""
+        self.join_offload()
         g, i = self.param_group[id(p)]
         a, n = g.offsets[i], g.numels[i]
         parts = []
-        for (s, e, og, moff, on_host) in g.runs:
-            lo, hi = g.seg_lo + s, g.seg_lo + e
+        for run in g.runs:
+            lo, hi = g.seg_lo + run[0], g.seg_lo + run[1]
             x0, x1 = max(lo, a), min(hi, a + n)
             if x0 < x1:
-                src = fetch(og, on_host)
+                src = self._run_read(g, run, key, x0 - g.seg_lo, x1 - g.seg_lo)
                 if src is not None:
-                    parts.append(src[moff + x0 - lo:moff + x1 - lo])
+                    parts.append(src)
         return torch.cat(parts).clone() if parts else None
 
     def get_full_fp32_param(self, p):
         """Gather the fp32 master value of one parameter (reference `safe_get_full_fp32_param`)."""
-        return self._gather_param(p, self._state_src("fp32"))
+        return self._gather_param(p, "fp32")
 
     def _ensure_state(self, key=None):
         """Materialise (zero) Adam moments for every optimizer group so they can be written into."""
         for og in range(len(self.fp32_flat)):
-            fp = self.fp32_flat[og]
-            st = self.optimizer.state[fp]
-            if len(st) == 0:
-                st["step"] = 0
-                st["exp_avg"] = torch.zeros_like(fp.data)
-                st["exp_avg_sq"] = torch.zeros_like(fp.data)
-            hp = self.master_host[og] if og < len(self.master_host) else None
-            if hp is not None and self.nvme_swapper is None and og not in self.host_states:
-                self.host_states[og] = [torch.zeros_like(hp), torch.zeros_like(hp), 0]
+            self._moments(og)
+            if self.off is not None:
+                self.off._ensure_moments(og)
 
     def set_step(self, step):
         for og in range(len(self.fp32_flat)):
             st = self.optimizer.state[self.fp32_flat[og]]
             if "step" in st:
                 st["step"] = int(step)
-        for st in self.host_states.values():
-            st[2] = int(step)
+            if self.off is not None:
+                self.off.step_count[og] = int(step)
 
     def get_full_optimizer_state(self, p, key):
-        return self._gather_param(p, self._state_src(key))
+        return self._gather_param(p, key)
 
     @torch.no_grad()
     def set_full_optimizer_state(self, p, value, key):
-        self._scatter_param(p, value, self._state_src(key))
+        self._scatter_param(p, value, key)
 
     def get_local_fp32_param(self, p):
-        return self._local_fragment(p, self._state_src("fp32"))
+        return self._local_fragment(p, "fp32")
 
     def get_local_optimizer_state(self, p, key):
-        return self._local_fragment(p, self._state_src(key))
+        return self._local_fragment(p, key)
 
     @torch.no_grad()
     def set_full_fp32_param(self, p, value):
         g, i = self.param_group[id(p)]
-        self._scatter_param(p, value, self._state_src("fp32"), also_shard=True)
+        self._scatter_param(p, value, "fp32", also_shard=True)
         if g.persistent and g.partition:
             dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
 
@@ -1021,9 +1100,17 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 seg32[g.offsets[i]:g.offsets[i] + g.numels[i]].copy_(p.grad.reshape(-1)).mul_(1.0 / self._div(g))
         elif g._acc_valid:
             for (s, e, og, moff, on_host) in g.runs:
-                seg32[s:e].copy_((self.grad_acc_host if on_host else self.grad_acc)[og][moff:moff + e - s])
+                if not on_host:
+                    seg32[s:e].copy_(self.grad_acc[og][moff:moff + e - s])
         elif g.red_out is not None:
             seg32.copy_(g.red_out).mul_(self._alpha(g))
+        for piece in g.pieces:  # offloaded runs: the gradient sits in its host staging slot / accumulator
+            if piece.covered and self.off is not None:
+                self.off._drain()
+                if self.off.cuda:
+                    self.off.d2h.synchronize()
+                src = self.off._grad_src(piece, piece.moff, piece.moff + piece.n)
+                seg32[piece.s:piece.s + piece.n].copy_(src.to(self.device, torch.float32)).mul_(piece.alpha)
         seg32.mul_(self._unscale_factor())
         if g.partition:
             full = torch.empty(g.padded, dtype=torch.float32, device=self.device)
@@ -1056,7 +1143,30 @@ class FlatZeroOptimizer(ZeROOptimizer):
         return out
 
     # ================================================================================ checkpoint state
+    def _device_master_fp32(self, og):
+        """fp32 master of og's device-resident elements (joined from weight + residual with split masters)."""
+        if not self.split_master:
+            return self.master[og].detach().cpu()
+        out = torch.zeros(self.master[og].numel(), dtype=torch.float32)
+        for g in self.groups:
+            for run in g.runs:
+                if run[2] == og and not run[4]:
+                    out[run[3]:run[3] + run[1] - run[0]].copy_(self._run_read(g, run, "fp32", run[0], run[1]))
+        return out
+
+    def _host_master_fp32(self, og):
+        if self.off is None or self.off.n[og] == 0:
+            return None
+        if not self.split_master:
+            return self.off.read_state(og, "fp32", 0, self.off.n[og]).clone()
+        out = torch.zeros(self.off.n[og], dtype=torch.float32)
+        for p in self.off.pieces[og]:
+            run = (p.s, p.s + p.n, og, p.moff, True)
+            out[p.moff:p.moff + p.n].copy_(self._run_read(p.group, run, "fp32", p.s, p.s + p.n))
+        return out
+
     def state_dict(self):
+        self.join_offload()
         sd = OrderedDict()
         sd[CK.ZERO_STAGE] = self.stage
         sd[CK.LOSS_SCALER] = self.loss_scaler.state_dict()
@@ -1065,23 +1175,27 @@ class FlatZeroOptimizer(ZeROOptimizer):
         sd[CK.CLIP_GRAD] = self.clip_grad
         sd[CK.PARTITION_COUNT] = self.partition_count()
         sd[CK.BASE_OPTIMIZER_STATE] = self.optimizer.state_dict()
-        sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS] = [m.detach().cpu() for m in self.master]
-        sd["fp32_host_partitions"] = [None if m is None else (m.read_full() if hasattr(m, "read_full") else
-                                                              m.detach().clone()) for m in self.master_host]
-        sd["host_optimizer_states"] = {og: [s[0].clone(), s[1].clone(), s[2]] for og, s in self.host_states.items()}
-        if self.nvme_swapper is not None:
-            for og in self.nvme_swapper.sizes:
-                m, v, st = self.nvme_swapper.read_full(og)
-                sd["host_optimizer_states"][og] = [m, v, st]
+        sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS] = [self._device_master_fp32(og) for og in range(self.num_og)]
+        sd["fp32_host_partitions"] = [self._host_master_fp32(og) for og in range(self.num_og)]
+        sd["host_optimizer_states"] = {}
+        if self.off is not None:
+            for og in range(self.num_og):
+                if self.off.n[og] and (self.off.step_count[og] or self.off.m[og] is not None):
+                    self.off._ensure_moments(og)
+                    n = self.off.n[og]
+                    sd["host_optimizer_states"][og] = [self.off.read_state(og, "exp_avg", 0, n).clone(),
+                                                       self.off.read_state(og, "exp_avg_sq", 0, n).clone(),
+                                                       self.off.step_count[og]]
         sd[CK.FLAT_LAYOUT] = self.layout()
         sd[CK.DS_VERSION] = _version()
         return sd
 
     @torch.no_grad()
     def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
+        self.join_offload()
         if load_optimizer_states:
             base = sd[CK.BASE_OPTIMIZER_STATE]
-            # our fp32 flat params are the optimizer params; restore states tensor-by-tensor onto device
+            # our flat params are the optimizer params; restore states tensor-by-tensor onto device
             saved_groups = base["param_groups"]
             for og, group in enumerate(self.optimizer.param_groups):
                 for k, v in saved_groups[og].items():
@@ -1095,12 +1209,11 @@ class FlatZeroOptimizer(ZeROOptimizer):
                     for k, v in st.items()
                 }
             for og, s in sd.get("host_optimizer_states", {}).items():
-                if self.nvme_swapper is not None:
-                    if int(og) not in self.nvme_swapper.sizes:
-                        self.nvme_swapper.register(int(og), s[0].numel())
-                    self.nvme_swapper.write_full(int(og), s[0], s[1], s[2])
-                else:
-                    self.host_states[int(og)] = [s[0].clone(), s[1].clone(), s[2]]
+                og = int(og)
+                if self.off is not None and self.off.n[og]:
+                    self.off.write_state(og, "exp_avg", 0, s[0])
+                    self.off.write_state(og, "exp_avg_sq", 0, s[1])
+                    self.off.step_count[og] = int(s[2])
         if CK.LOSS_SCALER in sd:
             ls = sd[CK.LOSS_SCALER]
             if isinstance(ls, dict):
@@ -1110,31 +1223,31 @@ class FlatZeroOptimizer(ZeROOptimizer):
         self.dynamic_loss_scale = sd.get("dynamic_loss_scale", self.dynamic_loss_scale)
         self.overflow = sd.get("overflow", False)
         if load_from_fp32_weights:
-            for og, m in enumerate(sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS]):
-                self.master[og].copy_(m.to(self.device))
-            for og, m in enumerate(sd.get("fp32_host_partitions", [])):
-                if m is not None and self.master_host[og] is not None:
-                    self.master_host[og].copy_(m)
-            # refresh low-precision shards from masters
+            dev = sd[CK.SINGLE_PARTITION_OF_FP32_GROUPS]
+            host = sd.get("fp32_host_partitions", [])
             for g in self.groups:
-                for (s, e, og, moff, on_host) in g.runs:
-                    src = (self.master_host if on_host else self.master)[og][moff:moff + e - s]
-                    g.shard[s:e].copy_(src.to(g.shard.device))
+                for run in g.runs:
+                    (s, e, og, moff, on_host) = run
+                    src = (host if on_host else dev)[og][moff:moff + e - s]
+                    self._run_write(g, run, "fp32", s, src.to(self.device), also_shard=True)
             self._post_step_gather()
 
     def refresh_from_module(self):
         """Re-read master weights from the (possibly externally modified) bf16 shards."""
+        self.join_offload()
         for g in self.groups:
-            for (s, e, og, moff, on_host) in g.runs:
-                _flat_write((self.master_host if on_host else self.master)[og], moff, g.shard[s:e].float())
+            for run in g.runs:
+                self._run_write(g, run, "fp32", run[0], g.shard[run[0]:run[1]].float().to(self.device))
 
 
-def _flat_write(dst, lo, t):
-    """dst[lo:lo + n] = t for a flat fp32 tensor or an NVMe-resident master (`NvmeFlat`)."""
-    if hasattr(dst, "write"):
-        dst.write(lo, t)
-    else:
-        dst[lo:lo + t.numel()].copy_(t)
+def _split_join(hi, lo):
+    from .offload import split_join
+    return split_join(hi.contiguous(), lo)
+
+
+def _split_cut(f32):
+    from .offload import split_cut
+    return split_cut(f32)
 
 
 class _nullctx:

@@ -24,10 +24,13 @@ def _zero3_linear_forward(self, x):
 
 
 def install_zero3_linear(module: nn.Module):
-    """Route every nn.Linear in `module` through LinearFunctionForZeroStage3 (idempotent)."""
+    """Route every nn.Linear in `module` through LinearFunctionForZeroStage3 (idempotent). Only layers whose forward
+    IS `nn.Linear.forward` are patched: a subclass with its own forward (compression layers that apply pruning masks
+    or quantisation, tensor-parallel row/column linears that all-reduce or gather) keeps it."""
     n = 0
     for m in module.modules():
-        if isinstance(m, nn.Linear) and not getattr(m, "_ds_zero3_linear", False):
+        if isinstance(m, nn.Linear) and type(m).forward is nn.Linear.forward and \
+                "forward" not in m.__dict__ and not getattr(m, "_ds_zero3_linear", False):
             m.forward = types.MethodType(_zero3_linear_forward, m)
             m._ds_zero3_linear = True
             n += 1

@@ -32,6 +32,11 @@ class DeepSpeedZeroOffloadOptimizerConfig(DeepSpeedConfigModel):
     fast_init: bool = False
     # ZeRO-Offload++ Twin-Flow: fraction of optimizer sub-groups stepped on the host (the rest on the GPU)
     ratio: float = Field(1.0, ge=0.0, le=1.0)
+    # MI355X additions. With device "nvme": number of offloaded elements whose state stays in host DRAM (the rest is
+    # streamed from NVMe), the optimizer-state analogue of offload_param.max_in_cpu.
+    max_in_cpu: int = Field(0, ge=0)
+    # let the next forward start while the host partition is still being stepped (modules wait for their own weights)
+    overlap_forward: bool = False
 
     @property
     def pipeline(self):

@@ -28,20 +28,23 @@ def _torch_ref(steps, lr):
     return out
 
 
-def _engine(stage, dtype, steps, lr, zero_extra=None):
+def _engine(stage, dtype, steps, lr, zero_extra=None, gas=1, split=False):
     import deepspeedsyclsupport_amd as ds
     from ..simple_model import base_config
     torch.manual_seed(0)
     m = tiny_llama(hidden_size=128, intermediate_size=256, num_attention_heads=4)
-    cfg = base_config(stage=stage, lr=lr, mb=2, clip=1.0, dtype=dtype)
+    cfg = base_config(stage=stage, lr=lr, mb=2, gas=gas, clip=1.0, dtype=dtype)
     cfg["zero_optimization"].update(zero_extra or {})
+    if split:
+        cfg["bf16"]["split_master_weights"] = True
     eng, _, _, _ = ds.initialize(model=m, config=cfg)
     out = []
-    for x in _data(steps, 5):
+    for x in _data(steps * gas, 5):
         loss = eng(x, labels=x)
         eng.backward(loss)
         eng.step()
         out.append(float(loss))
+    eng.optimizer.join_offload()
     return out
 
 
@@ -89,3 +92,68 @@ def test_partitioned_zeropp_on_one_gpu(monkeypatch):
     got = _engine(3, "bf16", 6, 3e-3, {"stage3_param_persistence_threshold": 0, "zero_quantized_weights": True,
                                        "zero_quantized_gradients": True})
     assert got == pytest.approx(ref, rel=5e-2, abs=5e-2), (got, ref)
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("ratio", [1.0, 0.4])
+def test_twin_flow_gpu_matches_device(ratio, overlap):
+    """ZeRO-Offload (ratio 1) / Twin-Flow on the device path: gradients staged to pinned memory on the d2h stream
+    during backward, native CPU Adam on the worker thread, weights back on the h2d stream — optionally with the next
+    forward overlapping the host step — must match the all-device optimizer."""
+    ref = _engine(3, "fp32", 5, 3e-3)
+    got = _engine(3, "fp32", 5, 3e-3, {"offload_optimizer": {"device": "cpu", "ratio": ratio, "pin_memory": True,
+                                                             "overlap_forward": overlap}})
+    assert got == pytest.approx(ref, rel=1e-4, abs=1e-4), (got, ref)
+
+
+def test_three_tier_offload_gpu(tmp_path):
+    """device + host DRAM + NVMe tail of optimizer state in one run, stepped through the pinned chunk pipeline."""
+    ref = _engine(3, "fp32", 4, 3e-3)
+    got = _engine(3, "fp32", 4, 3e-3, {"sub_group_size": 16384, "offload_optimizer": {
+        "device": "nvme", "ratio": 0.7, "max_in_cpu": 150000, "nvme_path": str(tmp_path), "pin_memory": True}})
+    assert got == pytest.approx(ref, rel=1e-4, abs=1e-4), (got, ref)
+
+
+@pytest.mark.parametrize("stage", [2, 3])
+def test_offload_gradient_accumulation_partitioned_gpu(stage, monkeypatch):
+    """gas 2 on the partitioned path: reduce-scattered segments go down through the bounce buffers into the fp32
+    host accumulator."""
+    monkeypatch.setenv("DS_ZERO_FORCE_PARTITION", "1")
+    ref = _engine(stage, "fp32", 3, 3e-3, {"stage3_param_persistence_threshold": 0}, gas=2)
+    got = _engine(stage, "fp32", 3, 3e-3, {"stage3_param_persistence_threshold": 0,
+                                           "offload_optimizer": {"device": "cpu", "ratio": 0.6, "pin_memory": True}},
+                  gas=2)
+    assert got == pytest.approx(ref, rel=1e-4, abs=1e-4), (got, ref)
+
+
+@pytest.mark.parametrize("offload", [None, {"device": "cpu", "ratio": 0.5, "pin_memory": True}])
+def test_split_master_weights_gpu(offload):
+    """bf16 weight + int16 residual masters (fused split Adam kernel on the device, split CPU Adam on the host)
+    follow the fp32-master bf16 run."""
+    ref = _engine(3, "bf16", 6, 3e-3)
+    extra = {"offload_optimizer": offload} if offload else None
+    got = _engine(3, "bf16", 6, 3e-3, extra, split=True)
+    assert got == pytest.approx(ref, rel=2e-2, abs=2e-2), (got, ref)
+
+
+def test_split_adam_kernel_matches_fp32_master():
+    """adam_multi_split == adam_multi on an fp32 master: join(hi, lo) equals the fp32 master after every step (same
+    fused arithmetic), on vector-aligned and odd-sized tensors."""
+    from deepspeedsyclsupport_amd.ops.native import hip_ops
+    from deepspeedsyclsupport_amd.runtime.zero.offload import split_cut, split_join
+    torch.manual_seed(0)
+    sizes = [8 * 4096 * 3, 1001]
+    ps = [(torch.randn(n, device="cuda") * 0.05) for n in sizes]
+    his, los = zip(*[split_cut(p) for p in ps])
+    his, los = [h.clone() for h in his], [l.clone() for l in los]
+    ms, vs = [torch.zeros_like(p) for p in ps], [torch.zeros_like(p) for p in ps]
+    ms2, vs2 = [torch.zeros_like(p) for p in ps], [torch.zeros_like(p) for p in ps]
+    for step in range(1, 5):
+        gs = [(torch.randn_like(p) * 1e-2).bfloat16() for p in ps]
+        lps = [torch.empty_like(p, dtype=torch.bfloat16) for p in ps]
+        bc1, bc2 = 1 - 0.9**step, 1 - 0.95**step
+        hip_ops().adam_multi(ps, ms, vs, gs, lps, 1e-2, 0.9, 0.95, 1e-8, 0.1, bc1, bc2, 0.5, True)
+        hip_ops().adam_multi_split(los, ms2, vs2, gs, his, 1e-2, 0.9, 0.95, 1e-8, 0.1, bc1, bc2, 0.5, True)
+        for p, hi, lo, m, m2 in zip(ps, his, los, ms, ms2):
+            assert torch.equal(split_join(hi, lo), p) and torch.equal(m, m2)
+            assert bool(((hi.float() - p).abs() <= p.abs() * 2.0**-8).all())
