@@ -182,7 +182,19 @@ class AioHandle {
     for (int64_t off = 0; off < len; off += chunk) {
       const int64_t n = std::min(chunk, len - off);
       const int64_t blk = block_;
-      futs.push_back(pool_.submit([=] { return do_io(fd, base + off, n, off, blk, write); }));
+      futs.push_back(pool_.submit([=]() -> int64_t {
+        int64_t r = do_io(fd, base + off, n, off, blk, write);
+        if (r < 0 && direct) {
+          // O_DIRECT refuses buffers the kernel cannot pin (e.g. memory mapped by the GPU driver): redo this part
+          // through the page cache
+          int fd2 = open_file(fn, write, false);
+          if (fd2 < 0) return r;
+          r = do_io(fd2, base + off, n, off, blk, write);
+          if (write) ::fsync(fd2);
+          ::close(fd2);
+        }
+        return r;
+      }));
     }
     if (async) {
       std::lock_guard<std::mutex> lk(mu_);

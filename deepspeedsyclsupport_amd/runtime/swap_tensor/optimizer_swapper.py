@@ -41,7 +41,12 @@ class OptimizerStateSwapper:
         return (n + _IO_ALIGN - 1) // _IO_ALIGN * _IO_ALIGN
 
     def _mk(self, dtype):
-        return torch.zeros(self.chunk, dtype=dtype, pin_memory=self.pin)
+        """Chunk buffers only ever meet the CPU optimizer and the file system (never a device copy), so they are
+        page-aligned, mlock'ed host memory from the aio engine: O_DIRECT can pin it, which it cannot do with memory
+        mapped by the GPU driver (hipHostMalloc)."""
+        t = self.sw.reader.new_cpu_locked_tensor(self.chunk, torch.empty(0, dtype=dtype))
+        t.zero_()
+        return t
 
     def _buffers(self):
         if self._bufs is None:
