@@ -11,6 +11,8 @@
 //    the Python side issues the H2D copy with `non_blocking=True` on a side HIP stream (Twin-Flow overlap).
 #include <torch/extension.h>
 
+#include <omp.h>
+
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -347,7 +349,14 @@ std::string simd_level() {
   return "scalar";
 }
 
+// OpenMP team size for the calling thread's later update calls (the Twin-Flow worker leaves a core to the thread
+// that launches GPU work when the host step overlaps the next forward)
+void cpu_set_omp_threads(int64_t n) { omp_set_num_threads((int)std::max<int64_t>(1, n)); }
+int64_t cpu_get_omp_threads() { return omp_get_max_threads(); }
+
 void register_cpu_optim(pybind11::module& m) {
+  m.def("cpu_set_omp_threads", &cpu_set_omp_threads);
+  m.def("cpu_get_omp_threads", &cpu_get_omp_threads);
   // the update loops run without the interpreter lock: the Twin-Flow worker thread steps the host partition while
   // the main thread launches the device optimizer and the next forward
   using nogil = pybind11::call_guard<pybind11::gil_scoped_release>;

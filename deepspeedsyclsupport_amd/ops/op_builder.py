@@ -101,7 +101,10 @@ def _write_ninja(names):
         "ninja_required_version = 1.3",
         f"hipcc = {hipcc}",
         "cxx = g++",
-        f"hipflags = --offload-arch={ARCH} -O3 -std=c++17 -fPIC -munsafe-fp-atomics -I{CSRC}/include",
+        # packed-fp32 VALU ops are disabled for all device code: hipcc -O3 forms them from ordinary float code and
+        # some of their forms have produced silently wrong results on this hardware pool
+        f"hipflags = --offload-arch={ARCH} -O3 -std=c++17 -fPIC -munsafe-fp-atomics -Xclang -target-feature "
+        f"-Xclang -packed-fp32-ops -I{CSRC}/include",
         f"cxxflags = -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI={abi} "
         f"-DTORCH_API_INCLUDE_EXTENSION_H " + " ".join(f"-isystem {p}" for p in inc) + f" -isystem {py_inc} "
         f"-isystem {rocm}/include -Wno-deprecated-declarations",

@@ -158,6 +158,12 @@ class DeepSpeedEngine(nn.Module):
                                    layer_num=c.eigenvalue_layer_num if c.eigenvalue_enabled else 0)
         if self.compression_scheduler is not None:
             self.compression_scheduler.moq_external = True
+        if self._zero3_partitioned():
+            # the step-time quantizer walks module.parameters(), which are empty placeholders once ZeRO-3 has
+            # partitioned them: it would silently quantize nothing
+            raise NotImplementedError("MoQ weight quantization after the optimizer step (quantize_weight_in_forward: "
+                                      "false) is not supported with partitioned ZeRO-3 parameters; use ZeRO stage "
+                                      "<= 2 or quantize_weight_in_forward: true")
 
     def _moq_quantize(self, block_eigenvalue=None):
         if self.quantizer is None or self.compression_scheduler is None or \
@@ -349,12 +355,27 @@ class DeepSpeedEngine(nn.Module):
             # coordinator installs the same function for partitioned runs)
             from .zero.linear import install_zero3_linear
             install_zero3_linear(self.module)
+        # sparse embedding gradients (reference `runtime/engine.py:325-327,2447-2518`): with `sparse_gradients` the
+        # weight gradient of every nn.Embedding / nn.EmbeddingBag travels as (row indices, rows) in an all-gather
+        # instead of a dense [vocab, hidden] reduction
+        sparse_params = set()
+        if self._config.sparse_gradients_enabled:
+            for name, m in self.module.named_modules():
+                if isinstance(m, (nn.Embedding, nn.EmbeddingBag)):
+                    self.sparse_tensor_module_names.add(name + ".weight")
+                    sparse_params.add(id(m.weight))
+                    log_dist(f"Will reduce the gradient of {name}.weight as a sparse tensor", ranks=[0])
+        comm_dtype = self._config.communication_data_type
+        if self.sequence_parallel_size > 1:
+            # reference `runtime/engine.py:1144-1145`: under Ulysses the gradient reduction over the sequence x data
+            # group runs in seq_parallel_communication_data_type (fp32 unless configured)
+            comm_dtype = self._config.seq_parallel_communication_data_type
         self.optimizer = FlatZeroOptimizer(basic, self.module, self._config, dp_group=self.seq_data_parallel_group,
                                            stage=stage, mpu=self.mpu, clip_grad=self.gradient_clipping(),
-                                           dtype=dtype,
-                                           communication_data_type=self._config.communication_data_type,
+                                           dtype=dtype, communication_data_type=comm_dtype,
                                            zero_config=self._config.zero_config, timers=None,
-                                           gradient_accumulation_steps=self.gradient_accumulation_steps())
+                                           gradient_accumulation_steps=self.gradient_accumulation_steps(),
+                                           sparse_params=sparse_params)
 
     def _configure_lr_scheduler(self, client_lr_scheduler):
         name = self._config.scheduler_name
@@ -461,15 +482,43 @@ class DeepSpeedEngine(nn.Module):
         self._is_gradient_accumulation_boundary = is_boundary
 
     # ============================================================================================ data
-    def deepspeed_io(self, dataset, batch_size=None, route=None, pin_memory=True, data_sampler=None, collate_fn=None,
-                     num_local_io_workers=None):
+    def curriculum_learning_enabled(self):
+        de = self._config.data_efficiency_config or {}
+        cl = de.get("data_sampling", {}).get("curriculum_learning", {})
+        return bool(de.get("enabled", False) and de.get("data_sampling", {}).get("enabled", False) and
+                    cl.get("enabled", False))
+
+    def deepspeed_io(self, dataset, batch_size=None, route="train", pin_memory=True, data_sampler=None,
+                     collate_fn=None, num_local_io_workers=None):
+        """Reference `runtime/engine.py:1686-1745`: the engine's loader over the data-parallel ranks; eval / predict
+        routes read in order; with `data_efficiency.data_sampling.curriculum_learning` on, batches come from the
+        curriculum `DeepSpeedDataSampler`."""
+        dp_world, dp_rank = self.dp_world_size, groups._get_data_parallel_rank()
+        if self.mpu is not None:
+            dp_world, dp_rank = self.mpu.get_data_parallel_world_size(), self.mpu.get_data_parallel_rank()
+        if data_sampler is None and route in ("predict", "eval"):
+            data_sampler = torch.utils.data.DistributedSampler(dataset, num_replicas=dp_world, rank=dp_rank,
+                                                               shuffle=False)
+        dl_config = {}
+        if self.curriculum_learning_enabled() and route == "train":
+            de = self._config.data_efficiency_config
+            dl_config = {"curriculum_learning": True, "data_efficiency": de,
+                         "data_parallel_group": groups._get_data_parallel_group(),
+                         "gradient_accumulation_steps": self.gradient_accumulation_steps(),
+                         "global_rank": self.global_rank,
+                         "data_sampling_num_workers": de.get("data_sampling", {}).get("num_workers", 0)}
         return DeepSpeedDataLoader(dataset, batch_size or self.train_micro_batch_size_per_gpu(),
-                                   pin_memory and self.device.type == "cuda", self.local_rank, self.tput_timer,
+                                   pin_memory and self.device.type == "cuda", self.local_rank,
+                                   self.tput_timer if route == "train" else None,
                                    collate_fn=collate_fn or self.collate_fn,
                                    num_local_io_workers=num_local_io_workers, data_sampler=data_sampler,
-                                   data_parallel_world_size=self.dp_world_size,
-                                   data_parallel_rank=groups._get_data_parallel_rank(),
-                                   dataloader_drop_last=self._config.dataloader_drop_last)
+                                   data_parallel_world_size=dp_world, data_parallel_rank=dp_rank,
+                                   dataloader_drop_last=self._config.dataloader_drop_last,
+                                   deepspeed_dataloader_config=dl_config)
+
+    def set_data_post_process_func(self, post_process_func):
+        if self.training_dataloader is not None:
+            self.training_dataloader.post_process_func = post_process_func
 
     # ============================================================================================ train loop
     def train(self, mode=True):
@@ -821,12 +870,14 @@ class DeepSpeedEngine(nn.Module):
         module_sd = dict(ck.get("module") or {})
         if getattr(self, "has_moe_layers", False):
             self._load_moe_experts(load_dir, tag, module_sd)
-        self._load_module_state(module_sd, strict=load_module_strict and not self._zero3_partitioned())
+        placeholders = self._load_module_state(module_sd, strict=load_module_strict)
         universal = bool(self._config.checkpoint_config.get("load_universal", False)) \
             if isinstance(self._config.checkpoint_config, dict) else \
             bool(getattr(self._config.checkpoint_config, "load_universal", False))
         # under partitioned ZeRO-3 the weights themselves live in the optimizer shards
-        need_shards = self.optimizer is not None and (not load_module_only or self._zero3_partitioned())
+        # (also when THIS engine does not partition but the checkpoint was saved partitioned: placeholders)
+        need_shards = self.optimizer is not None and (not load_module_only or self._zero3_partitioned() or
+                                                      bool(placeholders))
         if universal and need_shards:
             from ..checkpoint.ds_to_universal import load_universal_into
             load_universal_into(self.optimizer, self.module, tag_dir)
@@ -871,22 +922,38 @@ class DeepSpeedEngine(nn.Module):
 
     @torch.no_grad()
     def _load_module_state(self, sd, strict=True):
+        """Load a module state dict. Under ZeRO-3 the dict of a partitioned run holds empty placeholders for the
+        partitioned parameters (their values live in the optimizer shards): those names are returned so the caller
+        restores them from the shards; real shape mismatches and (with `strict`) missing keys raise."""
         if self.zero_optimization_partition_weights() and self.optimizer is not None:
             own = dict(self.module.named_parameters())
+            placeholders, bad = [], []
             for n, v in sd.items():
                 p = own.get(n)
-                # partitioned placeholders (numel 0) are restored from the optimizer shards instead
-                if p is not None and torch.is_tensor(v) and v.numel() == getattr(p, "ds_numel", p.numel()) and \
-                        v.numel() > 0:
+                if p is None or not torch.is_tensor(v):
+                    continue
+                want = getattr(p, "ds_numel", p.numel())
+                if v.numel() == want and v.numel() > 0:
                     self.optimizer.set_full_fp32_param(p, v.to(self.device))
+                elif v.numel() == 0 and want > 0:
+                    placeholders.append(n)
+                else:
+                    bad.append(f"{n}: checkpoint {tuple(v.shape)} vs model {tuple(getattr(p, 'ds_shape', p.shape))}")
+            if bad:
+                raise RuntimeError("size mismatch loading module state: " + "; ".join(bad[:5]))
+            if strict:
+                missing = [n for n in own if n not in sd]
+                if missing:
+                    raise RuntimeError(f"missing keys in checkpoint module state: {missing[:5]}")
             bufs = dict(self.module.named_buffers())
             for n, v in sd.items():
                 if n in bufs:
                     bufs[n].copy_(v)
-            return
+            return placeholders
         self.module.load_state_dict(sd, strict=strict)
         if self.optimizer is not None:
             self.optimizer.refresh_from_module()
+        return []
 
     def save_16bit_model(self, save_dir, save_filename="pytorch_model.bin", exclude_frozen_parameters=False):
         """Consolidated 16-bit weights, streamed group by group to rank 0 (reference `runtime/engine.py:3477`)."""

@@ -118,9 +118,11 @@ class FlatZeroOptimizer(ZeROOptimizer):
 
     def __init__(self, init_optimizer, module, ds_config, dp_group=None, stage=0, mpu=None, clip_grad=0.0,
                  dtype=torch.bfloat16, communication_data_type=None, zero_config=None, timers=None,
-                 gradient_accumulation_steps=1, expert_params=None):
+                 gradient_accumulation_steps=1, expert_params=None, sparse_params=None):
         self.optimizer = init_optimizer
         self.module = module
+        self.sparse_params = set(sparse_params or ())  # ids of embedding weights reduced as sparse tensors
+        self.sparse_reductions = 0
         self.stage = int(stage)
         self.zc = zero_config
         self.expert_grad_scaling = str(getattr(zero_config, "moe_expert_grad_scaling", "global") or "global")
@@ -247,6 +249,9 @@ class FlatZeroOptimizer(ZeROOptimizer):
                     continue
                 for p in ps:
                     owned.add(id(p))
+                for p in [p for p in ps if id(p) in self.sparse_params]:  # sparse-reduced weights: a group each
+                    groups.append(dict(params=[p], persistent=not fetched, module=m, sparse=True))
+                ps = [p for p in ps if id(p) not in self.sparse_params]
                 big = [p for p in ps if _pnumel(p) >= thr]
                 small = [p for p in ps if _pnumel(p) < thr]
                 persistent.extend(small)
@@ -264,6 +269,9 @@ class FlatZeroOptimizer(ZeROOptimizer):
             cap = int(self.zc.reduce_bucket_size) if self.zc is not None else int(5e8)
             cur, cur_n = [], 0
             for p in reversed(self.opt_params):
+                if id(p) in self.sparse_params:
+                    groups.append(dict(params=[p], persistent=True, module=None, sparse=True))
+                    continue
                 if cur and (cur_n + _pnumel(p) > cap or self.param_to_og[id(p)] != self.param_to_og[id(cur[-1])]):
                     groups.append(dict(params=cur, persistent=True, module=None))
                     cur, cur_n = [], 0
@@ -281,6 +289,7 @@ class FlatZeroOptimizer(ZeROOptimizer):
             g = FlatGroup(i, d["params"], gdp, grank, self.stage >= 1 and multi, persistent,
                           self.device, self.dtype, d["module"], dp_group=pg)
             g.expert = bool(self.optimizer.param_groups[og].get("moe", False))
+            g.sparse = bool(d.get("sparse", False))
             self.groups.append(g)
         self.param_group = {}
         import weakref
@@ -619,6 +628,9 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 comm.mul_(pre)
             if self._local_grads():
                 out = comm  # a communication-compressed optimizer (1-bit Adam/LAMB, 0/1 Adam) averages on its own
+            elif getattr(g, "sparse", False) and g.reduce_dp > 1:
+                comm = self._sparse_reduce(g, comm)
+                out = comm[g.seg_lo:g.seg_lo + g.seg]
             elif g.partition:
                 out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
                 if self.zc is not None and self.zc.zero_quantized_gradients:
@@ -642,6 +654,19 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 if self.rs_stream is not None:
                     src.record_stream(self.rs_stream)
                 g.grad_flat = None
+
+    def _sparse_reduce(self, g, flat):
+        """Sum a row-sparse embedding gradient over the group by all-gathering (row indices, rows) (reference
+        `runtime/engine.py:2462-2518` sparse_allreduce) and scatter-adding them back into the dense flat buffer."""
+        from ..sparse_tensor import SparseTensor, sparse_allreduce
+        p = g.params[0]
+        rows = p.ds_shape[0]
+        dense = flat[:g.numels[0]].view(rows, g.numels[0] // rows)
+        st = sparse_allreduce(SparseTensor(dense), group=g.dp_group, average=False)
+        flat.zero_()
+        dense.index_add_(0, st.indices, st.values)
+        self.sparse_reductions += 1
+        return flat
 
     def _alpha(self, g=None):
         """Factor still owed to the reduced gradient: 1 / (div * pre_factor)."""

@@ -109,6 +109,11 @@ class OffloadedState:
         self._worker = None
         self._jobs = queue.Queue()
         self._err = None
+        if self.overlap_forward:
+            # worker and main thread both run short Python sections between native calls; a short switch interval
+            # keeps either from waiting whole 5 ms slices for the interpreter lock
+            import sys
+            sys.setswitchinterval(min(sys.getswitchinterval(), 2e-4))
 
     # ---------------------------------------------------------------- allocation
     def _host(self, n, dtype):
@@ -323,6 +328,10 @@ class OffloadedState:
 
             def loop():
                 torch.cuda.set_device(dev)
+                if self.overlap_forward:
+                    # the main thread keeps launching the next forward while this thread steps: leave it a core
+                    from ...ops.native import cpu_ops
+                    cpu_ops().cpu_set_omp_threads(max(1, cpu_ops().cpu_get_omp_threads() - 1))
                 while True:
                     f = self._jobs.get()
                     if f is None:
