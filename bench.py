@@ -93,6 +93,53 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def causal_flops_per_token(cfg, seq_len):
+    return 6 * cfg.num_params() + 6 * cfg.num_hidden_layers * cfg.hidden_size * seq_len
+
+
+def forced_partition_loop(args, cfg, config, dev, batches, sync, steps=3, warmup=1):
+    """tokens/s of the same model and config with DS_ZERO_FORCE_PARTITION=1 (a fresh engine; the first one's memory
+    is released by the caller's references going away before this runs)."""
+    import gc
+
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd.models.llama import LlamaForCausalLM
+    main_engine = forced_partition_loop.release()
+    del main_engine
+    gc.collect()
+    torch.cuda.empty_cache()
+    os.environ["DS_ZERO_FORCE_PARTITION"] = "1"
+    try:
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(torch.bfloat16)
+        with torch.device(dev):
+            model = LlamaForCausalLM(cfg)
+        torch.set_default_dtype(prev)
+        if args.ckpt:
+            model.gradient_checkpointing_enable()
+        engine, _, _, _ = ds.initialize(model=model, config=config)
+        assert engine.optimizer.partition and engine.optimizer.coordinator is not None
+
+        def step(i):
+            x = batches[i % len(batches)]
+            loss = engine(x, labels=x)
+            engine.backward(loss)
+            engine.step()
+            return loss
+
+        for i in range(warmup):
+            step(i)
+        sync()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(warmup + i)
+        sync()
+        dt = time.perf_counter() - t0
+        return round(args.micro_batch * args.seq_len * steps / dt, 2)
+    finally:
+        os.environ["DS_ZERO_FORCE_PARTITION"] = "0"
+
+
 def main():
     args = parse()
     import deepspeedsyclsupport_amd as ds
@@ -226,6 +273,27 @@ def main():
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t)
 
+    # One data-parallel rank runs ZeRO-3 without partitioning (nothing to gather from): time a short second loop in
+    # this process with the partitioned code path forced on (per-module all-gather on the prefetch stream,
+    # reduce-scatter on the reduction stream, shard pointing), so the multi-rank machinery is measured at N=1 too.
+    forced = None
+    final_loss = float(loss)
+    holder = {"engine": engine, "model": model}
+
+    def release():
+        return holder.pop("engine", None), holder.pop("model", None)
+
+    forced_partition_loop.release = release
+    partitioned = bool(getattr(engine.optimizer, "partition", False))
+    if world == 1 and on_gpu and args.stage == 3 and not args.host_dryrun and \
+            os.environ.get("DS_ZERO_FORCE_PARTITION", "0") != "1" and os.environ.get("DS_BENCH_FORCED", "1") == "1":
+        try:
+            if args.gas == 1 and args.sp == 1 and args.offload_ratio == 0:
+                del engine, model, loss
+                forced = forced_partition_loop(args, cfg, config, dev, batches, sync)
+        except Exception as e:  # the headline number above stands on its own
+            log(f"[bench] forced-partition loop failed: {type(e).__name__}: {e}")
+
     ms_per_step = elapsed / args.steps * 1e3
     tokens_per_step = dp * args.micro_batch * args.gas * args.seq_len  # each sp group covers whole sequences
     tok_s = tokens_per_step * args.steps / elapsed
@@ -255,7 +323,7 @@ def main():
                 "zero_stage": args.stage,
                 # True when parameters / gradients really are partitioned and gathered / reduce-scattered in the
                 # timed steps (always with > 1 data-parallel rank; at one rank only with DS_ZERO_FORCE_PARTITION=1)
-                "zero_partitioned": bool(getattr(engine.optimizer, "partition", False)),
+                "zero_partitioned": partitioned,
                 "twin_flow_offload_ratio": args.offload_ratio,
                 "attention": "in-tree CDNA4 flash fwd+bwd (csrc/attn/flash_{fwd,bwd}.hip)",
                 "micro_batch_per_gpu": args.micro_batch,
@@ -264,11 +332,17 @@ def main():
                 "optimizer": "FusedAdam(AdamW, gfx950 kernel)",
             },
             "tokens_per_sec_per_gpu": round(tok_s / world, 2),
+            # model FLOPs with the usual full-attention convention (12*L*H*S per token), and with the causal mask
+            # accounted for (half of the score / context FLOPs are never computed)
             "model_tflops_per_gpu": round(tflops_gpu, 1),
             "mfu_vs_2.5PF_bf16_dense": round(tflops_gpu / 2500.0, 4),
+            "model_tflops_per_gpu_causal": round(tok_s * causal_flops_per_token(cfg, args.seq_len) / world / 1e12, 1),
+            "mfu_causal_vs_2.5PF_bf16_dense": round(tok_s * causal_flops_per_token(cfg, args.seq_len) / world / 2.5e15,
+                                                    4),
+            "forced_partition_tokens_per_sec": forced,
             "params": n_params,
             "peak_mem_gib_per_gpu": round(peak_mem, 1),
-            "final_loss": round(float(loss), 4),
+            "final_loss": round(final_loss, 4),
         }
         print(json.dumps(out), flush=True)
     dist.barrier()

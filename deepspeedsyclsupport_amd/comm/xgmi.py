@@ -48,6 +48,8 @@ class XgmiAllReduce:
             raise ValueError(f"xGMI all-reduce supports 2..{self.ext.xar_max_world()} ranks, got {self.world}")
         self.id = self.ext.xar_create(self.world, self.rank, cap_bytes)
         self.cap = self.ext.xar_cap(self.id)
+        if os.environ.get("DS_XGMI_AR_TIMEOUT_MS"):
+            self.set_timeout_ms(float(os.environ["DS_XGMI_AR_TIMEOUT_MS"]))
         handles = [None] * self.world
         tdist.all_gather_object(handles, self.ext.xar_handles(self.id), group=group)
         for p, h in enumerate(handles):
@@ -68,8 +70,13 @@ class XgmiAllReduce:
         return out
 
     def error(self, reset=False):
-        """0 if every wait completed; 1 + peer index of a wait that timed out (diagnostic, synchronises)."""
+        """0 if every wait completed; 1 + peer index of a wait that timed out (sticky; synchronises). A timed-out
+        call fills its output with NaN and every later `all_reduce` raises until the word is reset."""
         return self.ext.xar_error(self.id, reset)
+
+    def set_timeout_ms(self, ms):
+        """Wait limit of the in-kernel peer waits (default 5 s; DS_XGMI_AR_TIMEOUT_MS at construction)."""
+        self.ext.xar_set_timeout_ms(self.id, float(ms))
 
     def close(self):
         if self.id is not None:

@@ -15,6 +15,7 @@ int ds_xar_handles(void*, void*);
 int ds_xar_open(void*, int, const void*);
 int ds_xar_allreduce(void*, const void*, void*, long long, int, int, hipStream_t);
 int ds_xar_error(void*, int);
+void ds_xar_set_timeout_ms(void*, double);
 void ds_xar_destroy(void*);
 }
 
@@ -58,10 +59,15 @@ void xar_allreduce(int64_t id, torch::Tensor in, torch::Tensor out, int64_t mode
   if (in.scalar_type() == at::kBFloat16) dt = 1;
   else if (in.scalar_type() == at::kHalf) dt = 2;
   else TORCH_CHECK(in.scalar_type() == at::kFloat, "xar: fp32/bf16/fp16 only");
-  check(ds_xar_allreduce(get(id), in.data_ptr(), out.data_ptr(), in.numel(), dt, (int)mode,
-                         at::hip::getCurrentHIPStream().stream()),
-        "xar_allreduce");
+  const int rc = ds_xar_allreduce(get(id), in.data_ptr(), out.data_ptr(), in.numel(), dt, (int)mode,
+                                  at::hip::getCurrentHIPStream().stream());
+  TORCH_CHECK(rc != (int)hipErrorLaunchTimeOut,
+              "xGMI all-reduce: a peer did not arrive within the wait limit in an earlier call (error word ",
+              ds_xar_error(get(id), 0), " = 1 + peer index); that call's output was filled with NaN. The ranks "
+              "are out of step: fix the straggler, or raise DS_XGMI_AR_TIMEOUT_MS, then reset the communicator");
+  check(rc, "xar_allreduce");
 }
+void xar_set_timeout_ms(int64_t id, double ms) { ds_xar_set_timeout_ms(get(id), ms); }
 
 int64_t xar_error(int64_t id, bool reset) { return ds_xar_error(get(id), reset ? 1 : 0); }
 int64_t xar_cap(int64_t id) { return ds_xar_cap(get(id)); }
@@ -85,5 +91,6 @@ void register_comm_ops(pybind11::module& m) {
   m.def("xar_allreduce", &xar_allreduce);
   m.def("xar_error", &xar_error, py::arg("id"), py::arg("reset") = false);
   m.def("xar_cap", &xar_cap);
+  m.def("xar_set_timeout_ms", &xar_set_timeout_ms);
   m.def("xar_destroy", &xar_destroy);
 }

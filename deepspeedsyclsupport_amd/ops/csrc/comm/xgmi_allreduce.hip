@@ -17,8 +17,10 @@
 //  * block b always uses its own private slot, double-buffered by epoch parity: a rank can only reach epoch e+2 of
 //    block b after every peer signalled e+1 of block b, i.e. after every peer finished reading epoch e's slot;
 //  * flags are compared wrap-safe (a fast peer may already have written e+2 when a slow one looks for e+1);
-//  * every wait is bounded (~5 s of the 100 MHz wall clock): on timeout the block records an error word and leaves,
-//    so a broken peer can never leave waves spinning on the GPU.
+//  * every wait is bounded (5 s of the 100 MHz wall clock by default): on timeout the block records a sticky error
+//    word (in device memory and in a host-mapped word the launcher reads without synchronising), fills its part of
+//    the output with NaN and leaves — a broken or late peer can never leave waves spinning on the GPU, and a partial
+//    sum is never returned as if it were a result: the NaNs poison the consumer and the next call raises.
 // Stores to peers are ordinary vector stores; the flag release / acquire use system-scope atomics.
 #include "ds_hip.h"
 
@@ -29,14 +31,16 @@ namespace {
 constexpr int XAR_MAX_WORLD = 8;
 constexpr int XAR_BLOCKS = 64;       // fixed block -> slot mapping (see above)
 constexpr int XAR_THREADS = 512;
-constexpr long long XAR_TIMEOUT = 500000000LL;  // wall_clock64 ticks (100 MHz): 5 s
+constexpr long long XAR_TIMEOUT = 500000000LL;  // default wait limit in wall_clock64 ticks (100 MHz): 5 s
 
 struct XarCtx {
   char* buf[XAR_MAX_WORLD];          // every rank's exchange buffer (own at [rank])
   unsigned* flags[XAR_MAX_WORLD];    // every rank's flag array
   unsigned* meta;                    // own: epoch per block, then error word
+  unsigned* err_host;                // host-mapped copy of the error word (sticky)
   int rank, world;
   long long slot;                    // bytes of one (block, source) slot
+  long long timeout;                 // wait limit in wall-clock ticks
 };
 
 // buffer layout: [parity 2][block][area 2 (recv, gather)][source world][slot]
@@ -48,8 +52,11 @@ __device__ __forceinline__ int xar_flag(const XarCtx& c, int phase, int b, int s
   return (phase * XAR_BLOCKS + b) * c.world + src;
 }
 
-// raise flag (phase, b, my rank) in every peer, then wait for every peer's flag in my array
-__device__ __forceinline__ void xar_barrier(const XarCtx& c, int phase, int b, unsigned v) {
+// raise flag (phase, b, my rank) in every peer, then wait for every peer's flag in my array; returns false (for
+// the whole block) if a peer did not arrive within the limit
+__device__ __forceinline__ bool xar_barrier(const XarCtx& c, int phase, int b, unsigned v) {
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
   __threadfence_system();
   __syncthreads();
   const int t = threadIdx.x;
@@ -58,8 +65,10 @@ __device__ __forceinline__ void xar_barrier(const XarCtx& c, int phase, int b, u
     const unsigned* mine = c.flags[c.rank] + xar_flag(c, phase, b, t);
     const long long t0 = wall_clock64();
     while ((int)(__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - v) < 0) {
-      if (wall_clock64() - t0 > XAR_TIMEOUT) {
+      if (wall_clock64() - t0 > c.timeout) {
         __hip_atomic_store(c.meta + XAR_BLOCKS, 1u + (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(c.err_host, 1u + (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_out = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -67,6 +76,13 @@ __device__ __forceinline__ void xar_barrier(const XarCtx& c, int phase, int b, u
   }
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return timed_out == 0;
+}
+
+// all-ones is a NaN in fp32, bf16 and fp16: the output of a call whose peers did not all arrive
+__device__ __forceinline__ void xar_poison(uint4* dst, long long cnt) {
+  const uint4 nan = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+  for (long long i = threadIdx.x; i < cnt; i += XAR_THREADS) dst[i] = nan;
 }
 
 // one 16-byte unit of T: 4 fp32 or 8 bf16 / fp16 elements, summed in fp32
@@ -103,13 +119,17 @@ __global__ void __launch_bounds__(XAR_THREADS) xar_oneshot(XarCtx c, const T* in
     for (int p = 0; p < c.world; ++p)
       *reinterpret_cast<uint4*>(c.buf[p] + xar_off(c, par, b, 0, c.rank) + 16 * i) = val;
   }
-  xar_barrier(c, 0, b, v);
+  const bool ok = xar_barrier(c, 0, b, v);
   const char* mine = c.buf[c.rank];
   uint4* dst = reinterpret_cast<uint4*>(out) + lo;
-  for (long long i = threadIdx.x; i < cnt; i += XAR_THREADS) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < c.world; ++s) U16<T>::add(acc, mine + xar_off(c, par, b, 0, s) + 16 * i);
-    dst[i] = U16<T>::pack(acc);
+  if (ok) {
+    for (long long i = threadIdx.x; i < cnt; i += XAR_THREADS) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < c.world; ++s) U16<T>::add(acc, mine + xar_off(c, par, b, 0, s) + 16 * i);
+      dst[i] = U16<T>::pack(acc);
+    }
+  } else {
+    xar_poison(dst, cnt);
   }
   __syncthreads();
   if (threadIdx.x == 0) c.meta[b] = v;
@@ -135,7 +155,7 @@ __global__ void __launch_bounds__(XAR_THREADS) xar_twoshot(XarCtx c, const T* in
     char* d = c.buf[p] + xar_off(c, par, b, 0, c.rank);
     for (long long i = threadIdx.x; i < nv; i += XAR_THREADS) *reinterpret_cast<uint4*>(d + 16 * i) = src[s0 + i];
   }
-  xar_barrier(c, 0, b, v);
+  bool ok = xar_barrier(c, 0, b, v);
   {  // reduce my sub-chunk, push it to every peer's gather slot [gather][my rank], keep it in out
     const char* mine = c.buf[c.rank];
     const long long s0 = sub_lo(c.rank), nv = sub_n(c.rank);
@@ -148,13 +168,16 @@ __global__ void __launch_bounds__(XAR_THREADS) xar_twoshot(XarCtx c, const T* in
         if (p != c.rank) *reinterpret_cast<uint4*>(c.buf[p] + xar_off(c, par, b, 1, c.rank) + 16 * i) = val;
     }
   }
-  xar_barrier(c, 1, b, v);
+  ok = xar_barrier(c, 1, b, v) && ok;
   for (int s = 0; s < c.world; ++s) {
     if (s == c.rank) continue;
     const long long s0 = sub_lo(s), nv = sub_n(s);
     const char* g = c.buf[c.rank] + xar_off(c, par, b, 1, s);
     for (long long i = threadIdx.x; i < nv; i += XAR_THREADS) dst[s0 + i] = *reinterpret_cast<const uint4*>(g + 16 * i);
   }
+  __syncthreads();
+  if (!ok) xar_poison(dst, cnt);  // (peers that did get this rank's partial sub-chunk poison theirs as well: they
+                                  // waited for the same missing flags)
   __syncthreads();
   if (threadIdx.x == 0) c.meta[b] = v;
 }
@@ -165,6 +188,8 @@ struct XarComm {
   char* buf = nullptr;
   unsigned* flags = nullptr;
   unsigned* meta = nullptr;
+  unsigned* err_host = nullptr;      // pinned, device-mapped: sticky error word readable without synchronising
+  long long timeout = XAR_TIMEOUT;
   char* peer_buf[XAR_MAX_WORLD] = {};
   unsigned* peer_flags[XAR_MAX_WORLD] = {};
 };
@@ -190,6 +215,8 @@ extern "C" int ds_xar_create(int world, int rank, long long cap_bytes, void** ou
   hipError_t rc = hipExtMallocWithFlags((void**)&m->buf, buf_bytes(m), hipDeviceMallocUncached);
   if (rc == hipSuccess) rc = hipExtMallocWithFlags((void**)&m->flags, flag_bytes(m), hipDeviceMallocUncached);
   if (rc == hipSuccess) rc = hipMalloc((void**)&m->meta, (XAR_BLOCKS + 1) * sizeof(unsigned));
+  if (rc == hipSuccess) rc = hipHostMalloc((void**)&m->err_host, sizeof(unsigned), hipHostMallocMapped);
+  if (rc == hipSuccess) *m->err_host = 0;
   if (rc == hipSuccess) rc = hipMemset(m->flags, 0, flag_bytes(m));
   if (rc == hipSuccess) rc = hipMemset(m->meta, 0, (XAR_BLOCKS + 1) * sizeof(unsigned));
   if (rc == hipSuccess) rc = hipDeviceSynchronize();
@@ -197,6 +224,7 @@ extern "C" int ds_xar_create(int world, int rank, long long cap_bytes, void** ou
     (void)hipFree(m->buf);
     (void)hipFree(m->flags);
     (void)hipFree(m->meta);
+    if (m->err_host) (void)hipHostFree(m->err_host);
     delete m;
     return (int)rc;
   }
@@ -246,12 +274,16 @@ extern "C" int ds_xar_allreduce(void* h, const void* in, void* out, long long n,
     if (!m->peer_buf[p] || !m->peer_flags[p]) return (int)hipErrorNotInitialized;
   const int es = dtype == DS_F32 ? 4 : 2;
   if (n <= 0 || (n * es) % 16 || n * es > m->cap || (mode != 1 && mode != 2)) return (int)hipErrorInvalidValue;
+  // a wait of an earlier call timed out (its output was poisoned): refuse to go on until the caller resets
+  if (*static_cast<volatile unsigned*>(m->err_host) != 0) return (int)hipErrorLaunchTimeOut;
   XarCtx c;
   for (int p = 0; p < XAR_MAX_WORLD; ++p) {
     c.buf[p] = m->peer_buf[p];
     c.flags[p] = m->peer_flags[p];
   }
   c.meta = m->meta;
+  c.err_host = m->err_host;
+  c.timeout = m->timeout;
   c.rank = m->rank;
   c.world = m->world;
   c.slot = m->slot;
@@ -283,8 +315,17 @@ extern "C" int ds_xar_error(void* h, int reset) {
   auto* m = static_cast<XarComm*>(h);
   unsigned e = 0;
   if (hipMemcpy(&e, m->meta + XAR_BLOCKS, sizeof(e), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (reset) (void)hipMemset(m->meta + XAR_BLOCKS, 0, sizeof(unsigned));
+  if (e == 0) e = *static_cast<volatile unsigned*>(m->err_host);
+  if (reset) {
+    (void)hipMemset(m->meta + XAR_BLOCKS, 0, sizeof(unsigned));
+    *m->err_host = 0;
+  }
   return (int)e;
+}
+
+// wait limit of every later call, in milliseconds (tests of the failure path use a few ms)
+extern "C" void ds_xar_set_timeout_ms(void* h, double ms) {
+  static_cast<XarComm*>(h)->timeout = (long long)(ms * 1e5);  // 100 MHz wall clock
 }
 
 extern "C" void ds_xar_destroy(void* h) {
@@ -298,5 +339,6 @@ extern "C" void ds_xar_destroy(void* h) {
   (void)hipFree(m->buf);
   (void)hipFree(m->flags);
   (void)hipFree(m->meta);
+  (void)hipHostFree(m->err_host);
   delete m;
 }

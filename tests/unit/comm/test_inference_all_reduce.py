@@ -82,3 +82,54 @@ def test_xgmi_all_reduce_two_ranks_one_gpu():
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     run_distributed(_xgmi_run, 2, timeout=240)
+
+
+def _xgmi_timeout_run():
+    """A peer that arrives later than the wait limit: the waiting rank's kernel leaves on its own (bounded wait),
+    its output is all NaN (never a partial sum), the next call raises until the error word is reset, and after the
+    reset the two ranks are still in step. The condition is forced from the host (one rank sleeps before launching,
+    the other has a 20 ms limit); every kernel exits normally."""
+    import os
+    import time
+    from deepspeedsyclsupport_amd.comm.xgmi import XgmiAllReduce
+    from deepspeedsyclsupport_amd import comm as dist
+    if os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY") not in (None, "0"):
+        pytest.skip("needs dmabuf IPC")
+    torch.cuda.set_device(0)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    ar = XgmiAllReduce(None, cap_bytes=1 << 20)
+    x = torch.full((4096, ), float(rank + 1), dtype=torch.float32, device="cuda")
+    ar.all_reduce(x, mode=1)
+    torch.cuda.synchronize()
+    assert torch.all(x == 3.0) and ar.error() == 0
+    dist.barrier()
+    if rank == 0:
+        ar.set_timeout_ms(20.0)
+    else:
+        time.sleep(1.0)  # the straggler
+    y = torch.full((4096, ), float(rank + 1), dtype=torch.float32, device="cuda")
+    ar.all_reduce(y, mode=1)
+    torch.cuda.synchronize()
+    if rank == 0:
+        assert bool(torch.isnan(y).all()), y[:4]
+        assert ar.error() == 2  # 1 + index of the peer that was late
+        with pytest.raises(RuntimeError, match="did not arrive"):
+            ar.all_reduce(y, mode=1)
+        assert ar.error(reset=True) == 2 and ar.error() == 0
+        ar.set_timeout_ms(5000.0)
+    else:
+        assert torch.all(y == 3.0)  # the late rank found its peer's data and flag already there
+    dist.barrier()
+    z = torch.full((4096, ), float(rank + 1), dtype=torch.float32, device="cuda")
+    ar.all_reduce(z, mode=2)
+    torch.cuda.synchronize()
+    assert torch.all(z == 3.0), z[:4]
+    dist.barrier()
+    ar.close()
+
+
+@pytest.mark.gpu
+def test_xgmi_all_reduce_timeout_is_loud():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    run_distributed(_xgmi_timeout_run, 2, timeout=240)
