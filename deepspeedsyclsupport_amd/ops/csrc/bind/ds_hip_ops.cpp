@@ -32,6 +32,8 @@ int ds_ln_bwd(const void*, const void*, const void*, const float*, const float*,
               float*, int64_t, int, int, hipStream_t);
 int ds_gated_act_fwd(const void*, void*, int64_t, int, int, int, hipStream_t);
 int ds_gated_act_bwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+int ds_gated_act_fwd_t(const void*, void*, void*, int64_t, int64_t, int, int, int, hipStream_t);
+int ds_gated_act_bwd_t(const void*, const void*, void*, void*, int64_t, int64_t, int, int, int, hipStream_t);
 int ds_bias_act_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 int ds_bias_act_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 int ds_bias_residual(const void*, const void*, const void*, void*, int64_t, int, float, int, hipStream_t);
@@ -285,6 +287,40 @@ Tensor gated_act_bwd(Tensor dout, Tensor gu, int64_t act) {
   check(ds_gated_act_bwd(dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(), rows, I, (int)act, dcode(gu), stream()),
         "gated_act_bwd");
   return dgu;
+}
+
+// gated activation that also writes the token-contiguous copy [I, Tp] (Tp = rows rounded up to `pad`): returns
+// {out [.., I], outT [I, Tp]}
+std::vector<Tensor> gated_act_fwd_t(Tensor gu, int64_t act, int64_t pad) {
+  need(gu, "gu");
+  TORCH_CHECK(gu.element_size() == 2, "gated_act_fwd_t: 16-bit dtypes only");
+  const int I = (int)(gu.size(-1) / 2);
+  const int64_t rows = gu.numel() / (2 * I);
+  const int64_t Tp = (rows + pad - 1) / pad * pad;
+  TORCH_CHECK(rows % 8 == 0 && I % 8 == 0 && Tp % 8 == 0, "gated_act_fwd_t: rows / features multiples of 8");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I;
+  auto out = torch::empty(sizes, gu.options());
+  auto outT = torch::empty({(int64_t)I, Tp}, gu.options());
+  check(ds_gated_act_fwd_t(gu.data_ptr(), out.data_ptr(), outT.data_ptr(), rows, Tp, I, (int)act, dcode(gu), stream()),
+        "gated_act_fwd_t");
+  return {out, outT};
+}
+
+// returns {dgu [.., 2I], dguT [2I, Tp]}
+std::vector<Tensor> gated_act_bwd_t(Tensor dout, Tensor gu, int64_t act, int64_t pad) {
+  need(dout, "dout"); need(gu, "gu");
+  TORCH_CHECK(gu.element_size() == 2 && dout.scalar_type() == gu.scalar_type(), "gated_act_bwd_t: 16-bit dtypes");
+  const int I = (int)(gu.size(-1) / 2);
+  const int64_t rows = gu.numel() / (2 * I);
+  const int64_t Tp = (rows + pad - 1) / pad * pad;
+  TORCH_CHECK(rows % 8 == 0 && I % 8 == 0 && Tp % 8 == 0 && dout.numel() == rows * I, "gated_act_bwd_t: shapes");
+  auto dgu = torch::empty_like(gu);
+  auto dguT = torch::empty({(int64_t)2 * I, Tp}, gu.options());
+  check(ds_gated_act_bwd_t(dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), rows, Tp, I, (int)act,
+                           dcode(gu), stream()),
+        "gated_act_bwd_t");
+  return {dgu, dguT};
 }
 
 Tensor bias_act_fwd(Tensor x, OptT bias, int64_t act) {
@@ -623,6 +659,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("gated_act_fwd", &gated_act_fwd);
   m.def("gated_act_bwd", &gated_act_bwd);
+  m.def("gated_act_fwd_t", &gated_act_fwd_t);
+  m.def("gated_act_bwd_t", &gated_act_bwd_t);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("bias_residual", &bias_residual);

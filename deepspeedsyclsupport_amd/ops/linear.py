@@ -30,15 +30,36 @@ def _rows16(t):
     return t
 
 
-def weight_grad(go2d, x2d):
+def kmajor_wanted(rows, dtype):
+    """Should a producer of a [rows, n] linear operand also write its token-contiguous copy? (same test as the
+    weight-gradient GEMM's, so a copy is only made where it will be used)"""
+    return _ENABLED and rows >= KMAJOR_MIN_ROWS and rows % 8 == 0 and dtype in (torch.bfloat16, torch.float16)
+
+
+STATS = {"kmajor_from_producer": 0, "kmajor_transposed": 0}  # how the weight-gradient operands were obtained
+
+
+def _kmajor_of(t2d, given, Tp):
+    """The [n, Tp] token-contiguous copy of t2d [T, n]: the one its producer wrote (`given`) or a transpose pass."""
+    if given is not None and given.shape == (t2d.shape[1], Tp) and given.dtype == t2d.dtype:
+        STATS["kmajor_from_producer"] += 1
+        return given
+    from .native import hip_ops
+    STATS["kmajor_transposed"] += 1
+    return hip_ops().transpose16(_rows16(t2d), Tp)
+
+
+def weight_grad(go2d, x2d, go_kmajor=None, x_kmajor=None):
     """[T, out], [T, in] -> dW [out, in]. The K-major copies are zero-padded to a multiple of 256 tokens (e.g. the
-    LM head's 32760 shifted tokens -> 32768: measured 7.6 ms -> 5.0 ms for that GEMM)."""
-    if _kmajor_ok(go2d, x2d):
-        from .native import hip_ops
-        h = hip_ops()
-        Tp = -(-go2d.shape[0] // 256) * 256
-        got = h.transpose16(_rows16(go2d), Tp)   # [out, Tp]
-        xt = h.transpose16(_rows16(x2d), Tp)     # [in, Tp]
+    LM head's 32760 shifted tokens -> 32768: measured 7.6 ms -> 5.0 ms for that GEMM). `x2d` may be None when the
+    forward kept only `x_kmajor`."""
+    T = go2d.shape[0]
+    if x_kmajor is not None or _kmajor_ok(go2d, x2d):
+        Tp = -(-T // 256) * 256
+        got = _kmajor_of(go2d, go_kmajor, Tp)                                    # [out, Tp]
+        if x2d is None:
+            STATS["kmajor_from_producer"] += 1
+        xt = x_kmajor if x2d is None else _kmajor_of(x2d, x_kmajor, Tp)          # [in, Tp]
         return torch.mm(got, xt.t())
     return go2d.t().mm(x2d)
 
@@ -55,10 +76,17 @@ def input_grad(go2d, weight):
 
 
 class LinearFunction(torch.autograd.Function):
+    """y = x W^T + b. `x_kmajor` ([in, Tp], written by x's producer) replaces x in what is kept for backward: the
+    weight gradient is its only use, so the row-major activation is not kept alive at all."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias=None):
-        ctx.save_for_backward(x, weight, bias)
+    def forward(ctx, x, weight, bias=None, x_kmajor=None):
+        if x_kmajor is not None:
+            ctx.save_for_backward(x_kmajor, weight, bias)
+            ctx.kmajor_saved = True
+        else:
+            ctx.save_for_backward(x, weight, bias)
+            ctx.kmajor_saved = False
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -71,11 +99,15 @@ class LinearFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = input_grad(go2, weight.to(go.dtype)).view(*go.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
-            gw = weight_grad(go2, x.reshape(-1, x.shape[-1]).to(go.dtype))
+            go_t = getattr(go, "_ds_kmajor", None)  # written by the gradient's producer kernel, if it makes one
+            if ctx.kmajor_saved:
+                gw = weight_grad(go2, None, go_t, x.to(go.dtype))
+            else:
+                gw = weight_grad(go2, x.reshape(-1, x.shape[-1]).to(go.dtype), go_t)
         if bias is not None and ctx.needs_input_grad[2]:
             gb = go2.sum(0)
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
 def linear(x, weight, bias=None):
-    return LinearFunction.apply(x, weight, bias)
+    return LinearFunction.apply(x, weight, bias, getattr(x, "_ds_kmajor", None))

@@ -105,10 +105,38 @@ class _GatedActFn(torch.autograd.Function):
         return hip_ops().gated_act_bwd(dout.contiguous(), gu, ctx.act), None
 
 
+class _GatedActKMajorFn(torch.autograd.Function):
+    """Gated activation of a long token batch in training: the kernels also write the token-contiguous ("K-major")
+    copies that the neighbouring linears' weight-gradient GEMMs contract over — the output's for the consumer
+    (handed over as `out._ds_kmajor`), the input gradient's for the producer (`dgu._ds_kmajor`) — instead of leaving
+    them to a separate transpose pass (see `ops/linear.py`)."""
+
+    @staticmethod
+    def forward(ctx, gu, act):
+        ctx.act = act
+        ctx.save_for_backward(gu)
+        out, out_t = hip_ops().gated_act_fwd_t(gu, act, 256)
+        ctx.mark_non_differentiable(out_t)
+        return out, out_t
+
+    @staticmethod
+    def backward(ctx, dout, _unused=None):
+        (gu, ) = ctx.saved_tensors
+        dgu, dgu_t = hip_ops().gated_act_bwd_t(dout.contiguous(), gu, ctx.act, 256)
+        dgu._ds_kmajor = dgu_t
+        return dgu, None
+
+
 def gated_activation(gate_up, act="silu"):
     """[.., 2I] = [gate | up] -> act(gate) * up  (SwiGLU for act='silu', GEGLU for 'gelu')."""
     code = ACT_CODES[act]
     if gate_up.is_cuda and (gate_up.shape[-1] // 2) % 8 == 0:
+        from ..linear import kmajor_wanted
+        rows = gate_up.numel() // gate_up.shape[-1]
+        if gate_up.requires_grad and torch.is_grad_enabled() and kmajor_wanted(rows, gate_up.dtype):
+            out, out_t = _GatedActKMajorFn.apply(gate_up.contiguous(), code)
+            out._ds_kmajor = out_t
+            return out
         return _GatedActFn.apply(gate_up.contiguous(), code)
     g, u = gate_up.chunk(2, dim=-1)
     return reference.ACTS[code](g) * u

@@ -16,11 +16,12 @@ LinearFunctionForZeroStage3 = LinearFunction
 
 
 def zero3_linear_wrap(input, weight, bias=None):
-    return LinearFunctionForZeroStage3.apply(input, weight, bias)
+    return LinearFunctionForZeroStage3.apply(input, weight, bias, getattr(input, "_ds_kmajor", None))
 
 
 def _zero3_linear_forward(self, x):
-    return LinearFunctionForZeroStage3.apply(x, self.weight, self.bias)
+    # a producer kernel may have written x's token-contiguous copy for the weight-gradient GEMM (`_ds_kmajor`)
+    return LinearFunctionForZeroStage3.apply(x, self.weight, self.bias, getattr(x, "_ds_kmajor", None))
 
 
 def install_zero3_linear(module: nn.Module):
