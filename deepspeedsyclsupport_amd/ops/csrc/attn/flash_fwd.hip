@@ -25,6 +25,8 @@
 // natural-log LSE [B,H,S] in fp32 that the backward pass consumes.
 #include "ds_hip.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int D = 128;
@@ -39,6 +41,37 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+typedef __attribute__((address_space(3))) bf16x8_t lds_bf16x8;
+
+// LDS-DMA: every lane fetches 16 bytes from its own global address; they land at lds_base + 16 * lane. Issued from
+// inline asm on purpose: hipcc tracks its own global_load_lds builtins and then waits vmcnt(0) before every LDS read it
+// cannot prove disjoint from the DMA target, draining the prefetch. Out of its sight the DMA is ordered only by the
+// `s_waitcnt vmcnt(0)` + barrier at the end of each tile (see flash_bwd.hip for the same idiom).
+__device__ __forceinline__ void glds16(const void* g, const char* lds_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_char*)lds_base);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
+}
+// same with a wave-uniform 64-bit base (scalar registers) and a 32-bit per-lane byte offset
+__device__ __forceinline__ void glds16_s(const char* base, uint32_t voff, const char* lds_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_char*)lds_base);
+  const uint64_t sb = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)sb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+  const uint64_t ub = ((uint64_t)hi << 32) | lo;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(ub), "s"(dst)
+               : "memory");
+}
+
 // byte offset of 16-B chunk `ch` (0..15) of row `row` in a [64][128 x bf16] tile: 256-B rows, chunk index XORed with
 // a bijection of row mod 16 so both the row reads (32 consecutive rows, one chunk) and the 4-row transposed reads
 // touch distinct banks.
@@ -47,6 +80,19 @@ __device__ __forceinline__ int lds_off(int row, int ch) {
 }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+constexpr float RESCALE_LOG2 = 8.f;
+
+// two fp32 -> one dword of two bf16 (round to nearest even), lo in bits 0..15
+__device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
 
 // block-sparse LUT: tiles [lay_heads, nqb, max_tiles] (ascending 64-key tile ids), ntiles [lay_heads, nqb],
 // layout [lay_heads, nb, nb] (uint8, block granularity blk)
@@ -106,26 +152,60 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
 
   // LDS: [K0][K1][V0][V1][scratch]
   float* scratch = reinterpret_cast<float*>(smem + 4 * TILE_BYTES) + wid * 32;
+  const lds_char* s3 = (const lds_char*)smem;  // 32-bit LDS addressing: per-lane base + compile-time displacement
 
-  // staging: thread t moves chunks t, t+256, t+512, t+768 (row = c>>4, 16-B chunk = c&15) of both K and V
-  u32x4_t kreg[4], vreg[4];
-  auto stage_load = [&](int tile) {
+  // ------------------------------------------------------------------ K/V staging by LDS-DMA
+  // A 64-key tile of K (or V) is sixteen 1-KB pieces (4 rows each); wave w moves pieces w, w+4, w+8, w+12 of both
+  // with `global_load_lds_dwordx4`: no staging registers, no ds_write, and the transfer of tile j+1 runs under the
+  // MFMAs of tile j. Lane L of piece p lands at physical chunk L%16 of row 4p + L/16, so it fetches the logical
+  // chunk (L%16) ^ swizzle(row) — the image's XOR swizzle goes on the SOURCE address. The row's low four bits
+  // (4w + L/16) do not depend on the piece, so one 32-bit byte offset per lane serves all pieces of all tiles; the
+  // tile / piece part of the address is wave-uniform (scalar base). Only a ragged last tile builds clamped
+  // per-lane addresses.
+  const int drow = 4 * wid + (lane >> 4);
+  const int dch = (lane & 15) ^ (((drow & 3) << 2) | ((drow >> 2) & 3));
+  const uint32_t kdma = (uint32_t)((drow * kss + dch * 8) * 2);
+  const uint32_t vdma = (uint32_t)((drow * vss + dch * 8) * 2);
+  auto dma_tile = [&](int tile, int buf) {
+    if (tile * BN + BN <= Skv) {
+      const char* kb = reinterpret_cast<const char*>(Kp + (int64_t)tile * BN * kss);
+      const char* vb = reinterpret_cast<const char*>(Vp + (int64_t)tile * BN * vss);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cidx = tid + i * NTHR, row = cidx >> 4, ch = cidx & 15;
-      const int key = min(tile * BN + row, Skv - 1);
-      kreg[i] = *reinterpret_cast<const u32x4_t*>(Kp + (int64_t)key * kss + ch * 8);
-      vreg[i] = *reinterpret_cast<const u32x4_t*>(Vp + (int64_t)key * vss + ch * 8);
+      for (int i = 0; i < 4; ++i) {
+        glds16_s(kb + (int64_t)32 * i * kss, kdma, smem + buf * TILE_BYTES + 1024 * (wid + 4 * i));
+        glds16_s(vb + (int64_t)32 * i * vss, vdma, smem + (2 + buf) * TILE_BYTES + 1024 * (wid + 4 * i));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = min(tile * BN + 16 * i + drow, Skv - 1);
+        glds16(Kp + (int64_t)key * kss + dch * 8, smem + buf * TILE_BYTES + 1024 * (wid + 4 * i));
+        glds16(Vp + (int64_t)key * vss + dch * 8, smem + (2 + buf) * TILE_BYTES + 1024 * (wid + 4 * i));
+      }
     }
   };
-  auto stage_store = [&](int buf) {
+  // every wave: its own DMA pieces have landed (vmcnt) and its LDS reads are done (lgkmcnt), then the barrier
+  auto tile_barrier = [&]() { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  // ------------------------------------------------------------------ per-lane LDS read addresses
+  // K row reads: lds_off(32t + l32, 2kk + h) = kaddr[kk] + 8192 t; V transposed reads (lane geometry of
+  // ds_read_b64_tr_b16: lane reads row rb + gq, 16-B chunk 4dt + 2 colhalf + gch, byte gb):
+  // lds_off(32t + 16ss + 4h + 8hi + gq, ...) + gb = vaddr[hi][dt] + 256 (32t + 16ss). The XOR swizzle only involves
+  // the row's low four bits, so tile half, k-step and buffer are compile-time displacements (the ds offset field).
+  const int gq = (lane >> 2) & 3, gch = (lane >> 1) & 1, gb = 8 * (lane & 1), colhalf = (lane >> 4) & 1;
+  uint32_t kaddr[8], vaddr[2][4];
+  {
+    const int f = ((l32 & 3) << 2) | ((l32 >> 2) & 3);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cidx = tid + i * NTHR, row = cidx >> 4, ch = cidx & 15;
-      *reinterpret_cast<u32x4_t*>(smem + buf * TILE_BYTES + lds_off(row, ch)) = kreg[i];
-      *reinterpret_cast<u32x4_t*>(smem + (2 + buf) * TILE_BYTES + lds_off(row, ch)) = vreg[i];
+    for (int kk = 0; kk < 8; ++kk) kaddr[kk] = (uint32_t)(l32 * 256 + 16 * ((2 * kk + h) ^ f));
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+      const int row = 4 * h + 8 * hi + gq, g = ((row & 3) << 2) | ((row >> 2) & 3);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        vaddr[hi][dt] = (uint32_t)(2 * TILE_BYTES + row * 256 + 16 * ((dt * 4 + colhalf * 2 + gch) ^ g) + gb);
     }
-  };
+  }
 
   f32x16_t o[4];
 #pragma unroll
@@ -133,34 +213,62 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
+  const float rescale_thr = RESCALE_LOG2 / c;  // in raw score units
   const int qrow_lane = q0w + l32;  // the query row this lane's scores belong to
 
-  if (nt > 0) {  // uniform per workgroup (a sparse row block may have no tiles)
-    stage_load(tile_of(0));
-    stage_store(0);
-  }
-  __syncthreads();
+  // the Q fragments are the only loads hipcc tracks: retire them before the first DMA so its own counted waits
+  // never have to look past transfers it does not know about
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) asm volatile("" : : "v"(qf[kk]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nt > 0) dma_tile(tile_of(0), 0);  // uniform per workgroup (a sparse row block may have no tiles)
+  tile_barrier();
 
-  for (int j = 0; j < nt; ++j) {
-    const int cur = j & 1;
-    if (j + 1 < nt) stage_load(tile_of(j + 1));
+  // one tile; `cur` (the LDS buffer) is a compile-time constant so it folds into the displacements
+  auto tile_step = [&](int j, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    if (j + 1 < nt) dma_tile(tile_of(j + 1), cur ^ 1);
     const int k0 = tile_of(j) * BN;
     const bool active = !CAUSAL || k0 <= q0w + 31;
     if (active) {
-      const char* Kt = smem + cur * TILE_BYTES;
-      const char* Vt = smem + (2 + cur) * TILE_BYTES;
-      // ---------------- S^T = K . Q^T  (two 32-key halves)
+      // ---------------- S^T = K . Q^T  (two 32-key halves), K fragments read three MFMAs ahead: left to itself
+      // hipcc issued each ds_read right before its MFMA and waited lgkmcnt(0) in between, so every MFMA paid a
+      // full LDS round trip. The order is pinned with sched_barrier (VALU and SALU may cross, MFMA / LDS may not).
+      auto ldk = [&](int i) {
+        return *reinterpret_cast<const lds_bf16x8*>(s3 + kaddr[i & 7] + (cur * TILE_BYTES + (i >> 3) * 8192));
+      };
       f32x16_t s[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
+      {
+        bf16x8_t k0f = ldk(0), k1f = ldk(1), k2f = ldk(2);
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(Kt + lds_off(t * 32 + l32, 2 * kk + h));
-          s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[t], 0, 0, 0);
+        for (int i = 0; i < 16; ++i) {
+          bf16x8_t k3f;
+          if (i + 3 < 16) k3f = ldk(i + 3);
+          __builtin_amdgcn_sched_barrier(0x6);
+          s[i >> 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0f, qf[i & 7], s[i >> 3], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0x6);
+          k0f = k1f;
+          k1f = k2f;
+          k2f = k3f;
         }
       }
+      // V operand i = (dt, t, ss): both transposed reads of the 16-key x 32-column slab; the first two are issued
+      // here so they fly under the softmax arithmetic
+      auto ldv = [&](int i) {
+        const int dt = i >> 2, t = (i >> 1) & 1, ss = i & 1;
+        const int disp = cur * TILE_BYTES + (t * 32 + 16 * ss) * 256;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(s3 + vaddr[0][dt] + disp));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(s3 + vaddr[1][dt] + disp));
+        s16x8 vv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { vv[e] = lo[e]; vv[4 + e] = hi[e]; }
+        return __builtin_bit_cast(bf16x8_t, vv);
+      };
+      bf16x8_t v0f = ldv(0), v1f = ldv(1);
       // ---------------- block-sparse mask at the layout's granularity (this lane's query row vs the 64 keys)
       if constexpr (SPARSE) {
         const int qr = min(qrow_lane, S - 1);
@@ -193,11 +301,16 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
           }
       }
       // ---------------- online softmax (row = this lane's query; partner lane^32 holds the other 32 keys)
+      // row max: one v_max3 per register pair (fmaxf on MFMA outputs makes hipcc canonicalise every input first)
       float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));
+      for (int r = 0; r < 16; ++r) mx = max3f(mx, s[0][r], s[1][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
+      // deferred rescale: the running reference maximum only moves when the new maximum exceeds it by more than
+      // RESCALE_LOG2 in the exponent's units, so most tiles skip the rescale of O entirely; until then the
+      // probabilities are at most 2^RESCALE_LOG2 (exact in fp32, in range for bf16), and l / LSE use the same
+      // reference, so the result is unchanged.
+      const float m_new = mx > m_run + rescale_thr ? mx : m_run;
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       const float alpha = fast_exp2((m_run - m_use) * c);
       const float mc = m_use * c;
@@ -231,39 +344,34 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
         __builtin_amdgcn_wave_barrier();
       }
       // ---------------- O += P . V  (P straight from the score registers; V via transposed LDS reads)
+      // two probabilities per v_cvt_pk_bf16_f32 (hipcc lowers an element-wise fptrunc to one convert plus a
+      // v_perm per element, and the VALU issue slots are what this loop runs out of)
       bf16x8_t pa[2][2];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
+        for (int ss = 0; ss < 2; ++ss) {
+          u32x4_t pu;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) pa[t][ss][e] = (bf16)s[t][8 * ss + e];
-      const int gq = (lane >> 2) & 3;        // row within the 4-row block this lane addresses
-      const int gch = (lane >> 1) & 1;       // chunk within the 16-column group
-      const int gb = 8 * (lane & 1);         // byte within the chunk
-      const int colhalf = (lane >> 4) & 1;   // which 16 columns of the 32-column tile
+          for (int i = 0; i < 4; ++i) pu[i] = pack_bf16(s[t][8 * ss + 2 * i], s[t][8 * ss + 2 * i + 1]);
+          pa[t][ss] = __builtin_bit_cast(bf16x8_t, pu);
+        }
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int ch0 = dt * 4 + colhalf * 2 + gch;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int ss = 0; ss < 2; ++ss) {
-            const int rb = t * 32 + 16 * ss + 4 * h;
-            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4_t*)(Vt + lds_off(rb + gq, ch0) + gb));
-            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4_t*)(Vt + lds_off(rb + 8 + gq, ch0) + gb));
-            s16x8 vv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { vv[e] = lo[e]; vv[4 + e] = hi[e]; }
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[t][ss], __builtin_bit_cast(bf16x8_t, vv), o[dt], 0,
-                                                           0, 0);
-          }
+      for (int i = 0; i < 16; ++i) {
+        bf16x8_t v2f;
+        if (i + 2 < 16) v2f = ldv(i + 2);
+        __builtin_amdgcn_sched_barrier(0x6);
+        o[i >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[(i >> 1) & 1][i & 1], v0f, o[i >> 2], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0x6);
+        v0f = v1f;
+        v1f = v2f;
       }
     }
-    if (j + 1 < nt) stage_store(cur ^ 1);
-    __syncthreads();
+    tile_barrier();
+  };
+  for (int j = 0; j < nt; j += 2) {
+    tile_step(j, std::integral_constant<int, 0>{});
+    if (j + 1 < nt) tile_step(j + 1, std::integral_constant<int, 1>{});
   }
 
   // ------------------------------------------------------------------ epilogue: O / l, LSE
