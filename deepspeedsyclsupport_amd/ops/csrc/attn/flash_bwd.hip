@@ -34,6 +34,13 @@
 // Measured (tools/bench_flash_bwd.py, profiles/flash_bwd_bench_r2_final.jsonl): B8 H32 S4096 D128 causal 4.2-4.3 ms
 // (round-2 start: 4.58). SQ PMC of the round-2 start: ~29 % MFMA busy, ~9 VALU per MFMA -- the VALU issue slots, not
 // the matrix pipe, are what the trims above (packed converts, pre-scaled row constants, uniform mask skip) buy back.
+// Where the time goes now: the dQ sum. Every 32-row query tile receives one 16-KB fp32 tile-add per 256-key block it
+// meets: B8 H32 S4096 causal = 278.5k tile-adds = 4.56 GB of float atomics, and the memory-side atomic units retire
+// ~1.3 TB/s chip-wide (one 256-B wave-instruction per ~50 ns per CU), i.e. a 3.5 ms floor for the main kernel at
+// this key-block size whatever the MFMA loop does (measured 3.8 ms + 0.3 ms pre/post; 4 heads x 32k: floor 3.3 ms,
+// measured 3.9 + 0.3). Pipelining the S / dP operand reads two MFMAs ahead (round 3) therefore bought only 2 %.
+// Going below the floor needs fewer adds per dQ element (512 keys per workgroup: the dK/dV accumulators no longer
+// fit two waves per SIMD) or bf16 atomics (2-3x the rounding error on dQ) -- neither taken.
 // Tried and measured slower: dQ partial stores + a summing pass instead of atomics (5.5 ms), pairing heavy and light
 // key blocks across XCDs for few-head long sequences (32k: 5.0 vs 4.75 ms; the dispatcher balances heavy-first),
 // splitting long key blocks' query ranges over several workgroups with fp32 dK/dV atomics (4 heads x 32k: 6.7 vs
@@ -62,6 +69,8 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) bf16x8_t lds_bf16x8;
 typedef __attribute__((address_space(1))) void glob_void;
 
 // LDS-DMA: every lane fetches `size` bytes from its own global address; they land at lds_base + lane * size.
@@ -265,8 +274,13 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
   const int gq = (lane >> 2) & 3, gch = (lane >> 1) & 1, gb = 8 * (lane & 1), colhalf = (lane >> 4) & 1;
   const int ds_unit = 4 * colhalf + 2 * gch + (lane & 1);
   auto swz = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
-  // row reads: lds_off(l32, 2kk+h) = rbase + 32 * (kk ^ rtog)
-  int rbase = l32 * 256 + 16 * ((h ^ swz(l32)) & 1), rtog = swz(l32) >> 1;
+  // row reads (operands of S and dP): lds_off(l32, 2kk+h) for the eight k-steps, as 32-bit LDS addresses of this
+  // wave's K rows; the Q / dO tile rows of the ring buffer in use sit at a wave-uniform distance from them, so a
+  // tile's sixteen Q / dO reads cost eight adds in all and everything else is a compile-time displacement
+  const lds_char* s3 = (const lds_char*)smem;
+  uint32_t kaddr[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) kaddr[kk] = (uint32_t)((KPW * w + l32) * 256 + 16 * ((2 * kk + h) ^ swz(l32)));
   // transposed tile reads: lds_off(4h+8hi+gq, 4dt + 2colhalf + gch) + gb = tbase[hi] + 64 * (dt ^ ttog[hi])
   int tbase[2], ttog[2];
   // dQ: transposed reads of the K image and of the dS^T image (no toggle: 16-row steps)
@@ -305,7 +319,7 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
 
   for (int it = 0; it < n_it; ++it) {
     const int cur = it & 1, tb = it % NBUF;
-    asm volatile("" : "+v"(rbase), "+v"(rtog), "+v"(tbase[0]), "+v"(tbase[1]), "+v"(ttog[0]), "+v"(ttog[1]),
+    asm volatile("" : "+v"(tbase[0]), "+v"(tbase[1]), "+v"(ttog[0]), "+v"(ttog[1]),
                  "+v"(dwbase), "+v"(dwtog), "+v"(kqoff[0]), "+v"(kqoff[1]), "+v"(dsqoff[0]), "+v"(dsqoff[1]));
     int hq, qt;
     tile_at(it, hq, qt);
@@ -365,17 +379,36 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) { s[4 * g + i] = x[i]; dp[4 * g + i] = y[i]; }
       }
-      const char* Kc = Kimg + (KPW * w + 32 * c) * 256;
+      // Operand reads run two MFMAs ahead of their use (S: Q and K rows, dP: dO rows; V is in registers): left to
+      // itself hipcc issued each ds_read right before its MFMA with lgkmcnt(0) in between, so all sixteen MFMAs paid
+      // a full LDS round trip. sched_barrier pins the order (VALU / SALU may cross, MFMA / LDS may not).
+      {
+        const uint32_t qdelta = (uint32_t)(K_BYTES + tb * 2 * TILE - KPW * w * 256);  // wave-uniform
+        uint32_t qaddr[8];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(Qt + rbase + 32 * (kk ^ rtog));
-        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(Kc + rbase + 32 * (kk ^ rtog));
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf, s, 0, 0, 0);
-      }
+        for (int kk = 0; kk < 8; ++kk) qaddr[kk] = kaddr[kk] + qdelta;
+        auto ld_q = [&](int kk) { return *reinterpret_cast<const lds_bf16x8*>(s3 + qaddr[kk]); };
+        auto ld_o = [&](int kk) { return *reinterpret_cast<const lds_bf16x8*>(s3 + qaddr[kk] + TILE); };
+        auto ld_k = [&](int kk) { return *reinterpret_cast<const lds_bf16x8*>(s3 + kaddr[kk] + 32 * c * 256); };
+        bf16x8_t a0 = ld_q(0), b0 = ld_k(0), a1 = ld_q(1), b1 = ld_k(1);
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(Ot + rbase + 32 * (kk ^ rtog));
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[c][kk], dp, 0, 0, 0);
+        for (int i = 0; i < 16; ++i) {
+          bf16x8_t a2, b2;
+          if (i + 2 < 8) {
+            a2 = ld_q(i + 2);
+            b2 = ld_k(i + 2);
+          } else if (i + 2 < 16) {
+            a2 = ld_o(i + 2 - 8);
+          }
+          __builtin_amdgcn_sched_barrier(0x6);
+          if (i < 8) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, s, 0, 0, 0);
+          else dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, vf[c][i - 8], dp, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0x6);
+          a0 = a1;
+          b0 = b1;
+          a1 = a2;
+          b1 = b2;
+        }
       }
       // ---------------- P and dS, dS^T -> LDS (row = key, 8-B unit g*2+h holds queries 8g+4h .. +3)
       // P and dS in fp32, then packed two per instruction (v_cvt_pk_bf16_f32; hipcc lowers a vector fptrunc to one
