@@ -143,6 +143,13 @@ struct BwdArgs {
   const int* nqt;
   const uint8_t* layout;
   int maxt, lay_heads, nb, blk;
+  // additive score biases of the block-sparse path (see flash_fwd.hip SparseLut), any may be null
+  const float *kbias, *abias, *rpe;
+  int64_t kb_stride, ab_stride, rpe_hs, rpe_rs;
+  // 1 = kbias, 2 = abias, 4 = rpe are real; with any of them set the others point at one zero float and their
+  // strides and key multipliers (ab_km / rpe_km) are 0, so the kernel loads unconditionally (a uniform branch around
+  // these loads runs into a hipcc ROCm 7.2 code generation error)
+  int bias_flags, kb_km, ab_km, rpe_km;
   int dbg;  // experiment switches (DS_FLASH_BWD_DBG): 1 no atomics, 2 no dQ phase, 4 no dK/dV products, 8 no S/dP
 };
 
@@ -150,7 +157,7 @@ struct BwdArgs {
 // NW = 4: one wave per SIMD with the whole 512-register file (dK^T/dV^T of 64 keys = 256 accumulator registers),
 // every wave also computes one 32-column slice of the tile's dQ; NW = 8: two waves per SIMD, 32 keys each, waves
 // 0..3 compute dQ.
-template <int NW, bool CAUSAL, bool SPARSE>
+template <int NW, bool CAUSAL, bool SPARSE, int BIASED = 0>
 __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
   constexpr int NTHR = NW * 64, KPW = KB / NW, NC = KPW / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -416,7 +423,28 @@ __global__ void __launch_bounds__(NW * 64, 1) flash_bwd_kernel(BwdArgs a) {
       // the per-element select costs 4 VALU and the VALU issue slots are the co-bottleneck beside the MFMAs.
       float pf[16], df[16];
       const bool need_mask = keep[c] != 0xffffu;
-      if (__any(need_mask)) {
+      if constexpr (BIASED != 0) {
+        // P = exp2(c * S' + log2(e) * bias): the per-key bias is one constant per lane, attention-mask / relative
+        // position values are read per (query row, key) — consecutive lanes read consecutive keys of one row.
+        // BIASED == 1: per-key bias only (BERT padding masks); 2: all three terms.
+        const int mykey = min(kw0 + 32 * c + l32, S - 1);
+        const float l2e = 1.4426950408889634f;
+        const float kb = a.kbias[(int64_t)b * a.kb_stride + (int64_t)mykey * a.kb_km] * l2e;
+        const float* abp = a.abias + (int64_t)mykey * a.ab_km;
+        const float* rpp = a.rpe + (int64_t)hq * a.rpe_hs + (int64_t)mykey * a.rpe_km;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float bv = kb;
+          if constexpr (BIASED == 2) {
+            const int qr = min(q0 + crow(r, h), S - 1);
+            bv = fmaf(abp[(int64_t)qr * a.ab_stride] + rpp[(int64_t)qr * a.rpe_rs], l2e, bv);
+          }
+          float p = __builtin_amdgcn_exp2f(fmaf(s[r], a.c, bv));
+          if (!((keep[c] >> r) & 1u)) p = 0.f;
+          pf[r] = p;
+          df[r] = p * dp[r];
+        }
+      } else if (__any(need_mask)) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float p = __builtin_amdgcn_exp2f(s[r] * a.c);
@@ -629,23 +657,25 @@ __global__ void __launch_bounds__(256) flash_bwd_post_kernel(const float* __rest
   *reinterpret_cast<bf16x8*>(dq + bb * sb + hh * sh + (int64_t)q * ss + sub * 8) = r;
 }
 
-template <int NW, bool C, bool SP>
+template <int NW, bool C, bool SP, int BI = 0>
 int launch_main(const BwdArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<NW, C, SP>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<NW, C, SP, BI>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<NW>());
     attr = true;
   }
   const int nkb = (a.S + KB - 1) / KB;
   const int grid = a.B * a.Hk * nkb;
-  hipLaunchKernelGGL((flash_bwd_kernel<NW, C, SP>), dim3(grid), dim3(NW * 64), lds_bytes<NW>(), st, a);
+  hipLaunchKernelGGL((flash_bwd_kernel<NW, C, SP, BI>), dim3(grid), dim3(NW * 64), lds_bytes<NW>(), st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 
 template <int NW>
 int launch_mode(const BwdArgs& a, int mode, hipStream_t st) {
+  if (mode == 2 && a.bias_flags == 1) return launch_main<NW, false, true, 1>(a, st);
+  if (mode == 2 && a.bias_flags) return launch_main<NW, false, true, 2>(a, st);
   return mode == 1 ? launch_main<NW, true, false>(a, st)
                    : (mode == 2 ? launch_main<NW, false, true>(a, st) : launch_main<NW, false, false>(a, st));
 }
@@ -661,7 +691,9 @@ extern "C" int ds_flash_bwd(const void* q, const void* k, const void* v, const v
                             int Hk, int S, const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os,
                             const int64_t* dos, const int64_t* dqs, const int64_t* dks, const int64_t* dvs,
                             float scale, int mode, const int* qtiles, const int* nqt, const uint8_t* layout, int maxt,
-                            int lay_heads, int nb, int blk, hipStream_t st) {
+                            int lay_heads, int nb, int blk, int bias_flags, const float* kbias, int64_t kb_stride,
+                            const float* abias, int64_t ab_stride, const float* rpe, int64_t rpe_hs, int64_t rpe_rs,
+                            hipStream_t st) {
   if (Hk <= 0 || Hq % Hk != 0 || S <= 0 || B <= 0) return (int)hipErrorInvalidValue;
   if (mode == 2 && (qtiles == nullptr || nqt == nullptr || layout == nullptr || (lay_heads != 1 && lay_heads != Hq) ||
                     (blk != 16 && blk != 32 && blk != 64 && blk != 128) || nb * blk < S))
@@ -685,6 +717,13 @@ extern "C" int ds_flash_bwd(const void* q, const void* k, const void* v, const v
   a.scale = scale;
   { const char* e = getenv("DS_FLASH_BWD_DBG"); a.dbg = e ? atoi(e) : 0; }
   a.qtiles = qtiles; a.nqt = nqt; a.layout = layout; a.maxt = maxt; a.lay_heads = lay_heads; a.nb = nb; a.blk = blk;
+  // biases: block-sparse path only; with any bias present every pointer must be valid (see BwdArgs::bias_flags)
+  if (bias_flags && (mode != 2 || !kbias || !abias || !rpe)) return (int)hipErrorInvalidValue;
+  a.kbias = kbias; a.abias = abias; a.rpe = rpe;
+  a.bias_flags = bias_flags;
+  a.kb_km = bias_flags & 1; a.ab_km = (bias_flags >> 1) & 1; a.rpe_km = (bias_flags >> 2) & 1;
+  a.kb_stride = a.kb_km ? kb_stride : 0; a.ab_stride = a.ab_km ? ab_stride : 0;
+  a.rpe_hs = a.rpe_km ? rpe_hs : 0; a.rpe_rs = a.rpe_km ? rpe_rs : 0;
   int rc = launch_mode<8>(a, mode, st);
   if (rc) return rc;
   hipLaunchKernelGGL(flash_bwd_post_kernel, dim3(pgrid), dim3(256), 0, st, dqacc, (bf16*)dq, Hq, S, rows, dqs[0],

@@ -102,6 +102,12 @@ struct SparseLut {
   const int* qorder;  // [lay_heads, nqb] query blocks by descending tile count
   const uint8_t* layout;
   int max_tiles, lay_heads, nb, blk;
+  // additive biases on the scaled scores (reference `ops/sparse_attention/softmax.py:37-70`: key-padding mask,
+  // attention mask and relative position embedding are applied inside the sparse softmax); any may be null
+  const float* kbias;      // [B, Skv] per-key (key_padding_mask in additive form), row stride kb_stride
+  const float* abias;      // [S, Skv] shared by batch and heads (attn_mask in additive form), row stride ab_stride
+  const float* rpe;        // [H or 1, S, Skv] per head, head stride rpe_hs (0 = shared), row stride rpe_rs
+  int64_t kb_stride, ab_stride, rpe_hs, rpe_rs;
 };
 
 template <bool CAUSAL, bool SPARSE>
@@ -269,8 +275,40 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
         return __builtin_bit_cast(bf16x8_t, vv);
       };
       bf16x8_t v0f = ldv(0), v1f = ldv(1);
-      // ---------------- block-sparse mask at the layout's granularity (this lane's query row vs the 64 keys)
+      // ---------------- additive biases (key padding / attention mask / relative position), in raw score units
+      // (bias / scale), then the block-sparse mask at the layout's granularity (this lane's query row vs the 64 keys)
       if constexpr (SPARSE) {
+        if (lut.kbias != nullptr || lut.abias != nullptr || lut.rpe != nullptr) {
+          const float inv_scale = 1.f / scale;
+          const int qr = min(qrow_lane, S - 1);
+          const float* kbp = lut.kbias ? lut.kbias + (int64_t)b * lut.kb_stride : nullptr;
+          const float* abp = lut.abias ? lut.abias + (int64_t)qr * lut.ab_stride : nullptr;
+          const float* rpp = lut.rpe ? lut.rpe + (int64_t)hq * lut.rpe_hs + (int64_t)qr * lut.rpe_rs : nullptr;
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int key = k0 + t * 32 + 8 * g + 4 * h;  // four consecutive keys: registers 4g .. 4g+3
+              if (key + 3 < Skv) {
+                f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
+                if (kbp) bsum += *reinterpret_cast<const f32x4*>(kbp + key);
+                if (abp) bsum += *reinterpret_cast<const f32x4*>(abp + key);
+                if (rpp) bsum += *reinterpret_cast<const f32x4*>(rpp + key);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) s[t][4 * g + i] = fmaf(bsum[i], inv_scale, s[t][4 * g + i]);
+              } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  if (key + i >= Skv) continue;
+                  float bv = 0.f;
+                  if (kbp) bv += kbp[key + i];
+                  if (abp) bv += abp[key + i];
+                  if (rpp) bv += rpp[key + i];
+                  s[t][4 * g + i] = fmaf(bv, inv_scale, s[t][4 * g + i]);
+                }
+              }
+            }
+        }
         const int qr = min(qrow_lane, S - 1);
         const uint8_t* lrow = lut.layout + ((int64_t)lh * lut.nb + qr / lut.blk) * lut.nb;
         uint64_t allow = 0;
@@ -401,13 +439,13 @@ __global__ void __launch_bounds__(NTHR, 2) flash_fwd_kernel(
     LSE[((int64_t)b * Hq + hq) * S + qrow_lane] =
         l_tot > 0.f ? (m_run * c + __log2f(l_tot)) * 0.69314718055994531f : INFINITY;
   }
-  (void)scale;
 }
 
 template <bool C, bool SP>
 int launch(const bf16* q, const bf16* k, const bf16* v, bf16* o, float* lse, int B, int Hq, int Hk, int S, int Skv,
            const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os, float scale, hipStream_t st,
-           SparseLut lut = SparseLut{nullptr, nullptr, nullptr, nullptr, 0, 1, 0, 1}) {
+           SparseLut lut = SparseLut{nullptr, nullptr, nullptr, nullptr, 0, 1, 0, 1, nullptr, nullptr, nullptr, 0, 0,
+                                     0, 0}) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_fwd_kernel<C, SP>),
@@ -446,12 +484,18 @@ extern "C" int ds_flash_fwd_sparse(const void* q, const void* k, const void* v, 
                                    int Hk, int S, const int64_t* qs, const int64_t* ks, const int64_t* vs,
                                    const int64_t* os, float scale, const int* tiles, const int* ntiles,
                                    const int* qorder, const uint8_t* layout, int max_tiles, int lay_heads, int nb,
-                                   int blk, hipStream_t st) {
+                                   int blk, const float* kbias, int64_t kb_stride, const float* abias,
+                                   int64_t ab_stride, const float* rpe, int64_t rpe_hs, int64_t rpe_rs,
+                                   hipStream_t st) {
   if (Hk <= 0 || Hq % Hk != 0 || S <= 0 || blk <= 0 || nb * blk < S || max_tiles < 0 ||
       (lay_heads != 1 && lay_heads != Hq) || tiles == nullptr || ntiles == nullptr || qorder == nullptr ||
       layout == nullptr)
     return (int)hipErrorInvalidValue;
+  // bias rows are read four keys at a time
+  auto al = [](const float* p, int64_t st) { return p == nullptr || (((uintptr_t)p % 16) == 0 && st % 4 == 0); };
+  if (!al(kbias, kb_stride) || !al(abias, ab_stride) || !al(rpe, rpe_rs) || rpe_hs % 4) return (int)hipErrorInvalidValue;
   return launch<false, true>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, Hq, Hk, S, S, qs, ks,
                              vs, os, scale, st,
-                             SparseLut{tiles, ntiles, qorder, layout, max_tiles, lay_heads, nb, blk});
+                             SparseLut{tiles, ntiles, qorder, layout, max_tiles, lay_heads, nb, blk, kbias, abias,
+                                       rpe, kb_stride, ab_stride, rpe_hs, rpe_rs});
 }

@@ -51,11 +51,13 @@ int ds_flash_fwd(const void*, const void*, const void*, void*, float*, int, int,
                  const int64_t*, const int64_t*, const int64_t*, float, int, hipStream_t);
 int ds_flash_fwd_sparse(const void*, const void*, const void*, void*, float*, int, int, int, int, const int64_t*,
                         const int64_t*, const int64_t*, const int64_t*, float, const int*, const int*, const int*,
-                        const uint8_t*, int, int, int, int, hipStream_t);
+                        const uint8_t*, int, int, int, int, const float*, int64_t, const float*, int64_t, const float*,
+                        int64_t, int64_t, hipStream_t);
 int ds_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, float*, void*,
                  void*, void*, int, int, int, int, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                  const int64_t*, const int64_t*, const int64_t*, const int64_t*, float, int, const int*, const int*,
-                 const uint8_t*, int, int, int, int, hipStream_t);
+                 const uint8_t*, int, int, int, int, int, const float*, int64_t, const float*, int64_t, const float*,
+                 int64_t, int64_t, hipStream_t);
 int ds_transpose16(const void*, void*, int, int, int, int64_t, hipStream_t);
 int ds_xent_fwd(const void*, const int64_t*, float*, float*, int64_t, int, int64_t, int, float, int, hipStream_t);
 int ds_xent_bwd(const void*, const int64_t*, const float*, const float*, float, void*, int64_t, int, int64_t, int64_t,
@@ -533,8 +535,41 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, bool causal, double 
 
 // Block-sparse flash forward (non-causal; causality belongs to the layout). tiles int32 [LH, nqb, T], ntiles int32
 // [LH, nqb], layout uint8 [LH, nb, nb] at granularity blk; LH in {1, Hq}. Same q/k/v/o/lse contract as flash_fwd.
+// additive score biases of the block-sparse attention: kbias [B, S], abias [S, S], rpe [H or 1, S, S], fp32 device
+// tensors with unit last stride, 16-B aligned rows
+struct AttnBias {
+  const float *kb = nullptr, *ab = nullptr, *rp = nullptr;
+  int64_t kbs = 0, abs_ = 0, rhs = 0, rrs = 0;
+};
+AttnBias attn_bias(const OptT& kbias, const OptT& abias, const OptT& rpe, int64_t B, int64_t H, int64_t S) {
+  AttnBias r;
+  auto chk = [](const Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.stride(-1) == 1 &&
+                    reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n, ": fp32 device tensor, unit last stride, "
+                "16-B aligned");
+  };
+  if (kbias.has_value() && kbias->defined()) {
+    chk(*kbias, "kbias");
+    TORCH_CHECK(kbias->dim() == 2 && kbias->size(0) == B && kbias->size(1) == S && kbias->stride(0) % 4 == 0, "kbias [B, S]");
+    r.kb = kbias->data_ptr<float>(); r.kbs = kbias->stride(0);
+  }
+  if (abias.has_value() && abias->defined()) {
+    chk(*abias, "abias");
+    TORCH_CHECK(abias->dim() == 2 && abias->size(0) == S && abias->size(1) == S && abias->stride(0) % 4 == 0, "abias [S, S]");
+    r.ab = abias->data_ptr<float>(); r.abs_ = abias->stride(0);
+  }
+  if (rpe.has_value() && rpe->defined()) {
+    chk(*rpe, "rpe");
+    TORCH_CHECK(rpe->dim() == 3 && (rpe->size(0) == H || rpe->size(0) == 1) && rpe->size(1) == S && rpe->size(2) == S &&
+                    rpe->stride(1) % 4 == 0 && rpe->stride(0) % 4 == 0, "rpe [H or 1, S, S]");
+    r.rp = rpe->data_ptr<float>(); r.rhs = rpe->size(0) == 1 ? 0 : rpe->stride(0); r.rrs = rpe->stride(1);
+  }
+  return r;
+}
+
 std::vector<Tensor> flash_fwd_sparse(Tensor q, Tensor k, Tensor v, double scale, Tensor tiles, Tensor ntiles,
-                                     Tensor qorder, Tensor layout, int64_t blk, bool want_lse) {
+                                     Tensor qorder, Tensor layout, int64_t blk, bool want_lse, OptT kbias,
+                                     OptT abias, OptT rpe) {
   TORCH_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "flash_fwd_sparse: device tensors expected");
   TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "flash_fwd_sparse: 4-D [B,H,S,D] tensors expected");
   TORCH_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 && v.scalar_type() == at::kBFloat16,
@@ -563,12 +598,14 @@ std::vector<Tensor> flash_fwd_sparse(Tensor q, Tensor k, Tensor v, double scale,
   auto o = torch::empty({B, S, Hq, 128}, q.options()).transpose(1, 2);
   Tensor lse;
   if (want_lse) lse = torch::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  const AttnBias ab = attn_bias(kbias, abias, rpe, B, Hq, S);
   const int64_t qs[3] = {q.stride(0), q.stride(1), q.stride(2)}, ks[3] = {k.stride(0), k.stride(1), k.stride(2)},
                 vs[3] = {v.stride(0), v.stride(1), v.stride(2)}, os[3] = {o.stride(0), o.stride(1), o.stride(2)};
   check(ds_flash_fwd_sparse(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
                             want_lse ? lse.data_ptr<float>() : nullptr, (int)B, (int)Hq, (int)Hk, (int)S, qs, ks, vs,
                             os, (float)scale, tiles.data_ptr<int>(), ntiles.data_ptr<int>(), qorder.data_ptr<int>(),
-                            layout.data_ptr<uint8_t>(), (int)tiles.size(2), (int)LH, (int)nb, (int)blk, stream()),
+                            layout.data_ptr<uint8_t>(), (int)tiles.size(2), (int)LH, (int)nb, (int)blk, ab.kb, ab.kbs,
+                            ab.ab, ab.abs_, ab.rp, ab.rhs, ab.rrs, stream()),
         "flash_fwd_sparse");
   return {o, lse};
 }
@@ -578,7 +615,8 @@ std::vector<Tensor> flash_fwd_sparse(Tensor q, Tensor k, Tensor v, double scale,
 // [Hk, nkb, T] of (head-in-group << 16 | 32-row tile), nqt int32 [Hk, nkb], layout uint8 [LH, nb, nb], granularity
 // blk). Returns dq, dk, dv laid out [B,S,H,128] in memory (viewed [B,H,S,128]) like flash_fwd's output.
 std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dout, double scale,
-                              int64_t mode, OptT qtiles, OptT nqt, OptT layout, int64_t blk) {
+                              int64_t mode, OptT qtiles, OptT nqt, OptT layout, int64_t blk, OptT kbias, OptT abias,
+                              OptT rpe) {
   for (const Tensor* t : {&q, &k, &v, &o, &dout}) {
     TORCH_CHECK(t->is_cuda() && t->dim() == 4 && t->scalar_type() == at::kBFloat16, "flash_bwd: 4-D bf16 device tensors");
     TORCH_CHECK(t->size(3) == 128 && t->stride(3) == 1, "flash_bwd: head dim 128 with unit last stride");
@@ -615,6 +653,13 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse
     }
     qt = qtiles->data_ptr<int>(); nq = nqt->data_ptr<int>(); lay = layout->data_ptr<uint8_t>();
   }
+  const AttnBias ab = attn_bias(kbias, abias, rpe, B, Hq, S);
+  TORCH_CHECK(mode == 2 || (!ab.kb && !ab.ab && !ab.rp), "flash_bwd: score biases need the block-sparse mode");
+  // the kernel loads all three bias terms unconditionally: absent ones read one zero float
+  const int flags = (ab.kb ? 1 : 0) | (ab.ab ? 2 : 0) | (ab.rp ? 4 : 0);
+  Tensor zero1;
+  if (flags) zero1 = torch::zeros({4}, q.options().dtype(at::kFloat));
+  auto zp = [&](const float* p) { return (p || !flags) ? p : zero1.data_ptr<float>(); };
   auto mk = [&](int64_t H) { return torch::empty({B, S, H, 128}, q.options()).transpose(1, 2); };
   auto dq = mk(Hq), dk = mk(Hk), dv = mk(Hk);
   auto delta = torch::empty({2 * B * Hq * S}, q.options().dtype(at::kFloat));  // -delta and -LSE/scale rows
@@ -625,7 +670,8 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse
   check(ds_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                      delta.data_ptr<float>(), dqacc.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                      (int)B, (int)Hq, (int)Hk, (int)S, qs, ks, vs, os, gs, dqs, dks, dvs, (float)scale, (int)mode, qt,
-                     nq, lay, maxt, LH, nb, (int)blk, stream()),
+                     nq, lay, maxt, LH, nb, (int)blk, flags, zp(ab.kb), ab.kbs, zp(ab.ab), ab.abs_, zp(ab.rp), ab.rhs,
+                     ab.rrs, stream()),
         "flash_bwd");
   return {dq, dk, dv};
 }
@@ -673,10 +719,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_inplace", &rope_inplace);
   m.def("transpose16", &transpose16, py::arg("x"), py::arg("pad_to") = 0);
   m.def("flash_fwd", &flash_fwd);
-  m.def("flash_fwd_sparse", &flash_fwd_sparse);
+  m.def("flash_fwd_sparse", &flash_fwd_sparse, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"),
+        py::arg("tiles"), py::arg("ntiles"), py::arg("qorder"), py::arg("layout"), py::arg("blk"), py::arg("want_lse"),
+        py::arg("kbias") = py::none(), py::arg("abias") = py::none(), py::arg("rpe") = py::none());
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"),
         py::arg("dout"), py::arg("scale"), py::arg("mode"), py::arg("qtiles") = py::none(), py::arg("nqt") = py::none(),
-        py::arg("layout") = py::none(), py::arg("blk") = 0);
+        py::arg("layout") = py::none(), py::arg("blk") = 0, py::arg("kbias") = py::none(),
+        py::arg("abias") = py::none(), py::arg("rpe") = py::none());
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
 }

@@ -104,9 +104,12 @@ def token_bias(layout, blk, L, H, dtype, device):
 
 
 class BlockSparseAttnFn(torch.autograd.Function):
+    """q/k/v bf16 [B, H, L, D], L a multiple of 128; kbias [B, L] / abias [L, L] / rpe [H or 1, L, L] are optional
+    fp32 additive biases on the scaled scores, applied inside the kernels (no gradient flows to them, as in the
+    reference's sparse softmax)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, layout, blk, scale):
+    def forward(ctx, q, k, v, layout, blk, scale, kbias, abias, rpe):
         B, H, L, D = q.shape
         tiles, ntiles, lay_u8, qorder = build_lut(layout, blk, L, q.device)
         if D < 128:
@@ -116,18 +119,21 @@ class BlockSparseAttnFn(torch.autograd.Function):
             qp, kp, vp = q, k, v
         need_grad = any(t.requires_grad for t in (q, k, v))
         o, lse = hip_ops().flash_fwd_sparse(qp, kp, vp, float(scale), tiles, ntiles, qorder, lay_u8, int(blk),
-                                              need_grad)
+                                              need_grad, kbias, abias, rpe)
         o_full = o
         if D < 128:
             o = o[..., :D]
         if need_grad:
-            ctx.save_for_backward(q, k, v, o_full, lse)
+            ctx.save_for_backward(q, k, v, o_full, lse, *[t for t in (kbias, abias, rpe) if t is not None])
+            ctx.has_bias = (kbias is not None, abias is not None, rpe is not None)
             ctx.layout, ctx.blk, ctx.scale = layout, blk, float(scale)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse = ctx.saved_tensors
+        q, k, v, o, lse, *bias = ctx.saved_tensors
+        it = iter(bias)
+        kbias, abias, rpe = (next(it) if has else None for has in ctx.has_bias)
         B, H, L, D = q.shape
         qtiles, nqt, lay_u8, blk = build_bwd_lut(ctx.layout, ctx.blk, L, H, q.device)
         if D < 128:
@@ -135,22 +141,64 @@ class BlockSparseAttnFn(torch.autograd.Function):
             q, k, v, do = (torch.nn.functional.pad(t, pad) for t in (q, k, v, do))
         elif do.stride(-1) != 1 or any(s % 8 for s in do.stride()[:3]):
             do = do.contiguous()
-        dq, dk, dv = hip_ops().flash_bwd(q, k, v, o, lse, do, ctx.scale, 2, qtiles, nqt, lay_u8, blk)
+        dq, dk, dv = hip_ops().flash_bwd(q, k, v, o, lse, do, ctx.scale, 2, qtiles, nqt, lay_u8, blk, kbias, abias, rpe)
         if D < 128:
             dq, dk, dv = dq[..., :D], dk[..., :D], dv[..., :D]
-        return dq, dk, dv, None, None, None
+        return dq, dk, dv, None, None, None, None, None, None
 
 
-def native_ok(q, k, v, blk, rpe=None, key_padding_mask=None, attn_mask=None):
+def native_ok(q, k, v, blk):
+    """Can the gfx950 block-sparse kernels take these tensors? (16-bit device tensors, same shapes, head dim <= 128;
+    fp16 runs in bf16; sequence lengths that are not a multiple of 128 are padded with masked keys)"""
     B, H, L, D = q.shape
-    return (q.is_cuda and q.dtype == torch.bfloat16 and k.dtype == q.dtype and v.dtype == q.dtype
-            and k.shape == q.shape and v.shape == q.shape and D <= 128 and D % 8 == 0 and L % 128 == 0
-            and L % blk == 0 and blk in (16, 32, 64, 128, 256) and rpe is None and key_padding_mask is None
-            and attn_mask is None and all(t.stride(-1) == 1 and all(x % 8 == 0 for x in t.stride()[:3])
-                                          for t in (q, k, v)))
+    return (q.is_cuda and q.dtype in (torch.bfloat16, torch.float16) and k.dtype == q.dtype and v.dtype == q.dtype
+            and k.shape == q.shape and v.shape == q.shape and D <= 128 and D % 8 == 0 and L % blk == 0
+            and blk in (16, 32, 64, 128, 256))
 
 
-def block_sparse_attention(q, k, v, layout, blk, scale=None):
-    """q/k/v [B, H, L, D] bf16, layout [H or 1, L/blk, L/blk] -> softmax(QK^T*scale masked by layout) V."""
-    scale = q.shape[-1]**-0.5 if scale is None else scale
-    return BlockSparseAttnFn.apply(q, k, v, layout, blk, scale)
+def _additive(mask, mode, shape_tail):
+    """Mask in 'add' mode is added as is; in 'mul' mode 0 drops (-inf) and anything else keeps (0)."""
+    m = mask.to(torch.float32)
+    if mode == "mul":
+        m = torch.where(m != 0, torch.zeros_like(m), torch.full_like(m, float("-inf")))
+    return m.reshape(*shape_tail)
+
+
+def block_sparse_attention(q, k, v, layout, blk, scale=None, key_padding_mask=None, attn_mask=None, rpe=None,
+                           key_padding_mask_mode="add", attn_mask_mode="mul"):
+    """q/k/v [B, H, L, D] bf16 (fp16 accepted: computed in bf16), layout [H or 1, L/blk, L/blk] ->
+    softmax(QK^T*scale + rpe + key_padding_mask + attn_mask, masked by layout) V. The masks and the relative
+    position embedding are applied inside the kernels (reference `ops/sparse_attention/softmax.py:37-157`); no
+    [B, H, L, L] tensor is built. L only needs to be a multiple of the block size: it is padded to a multiple of 128
+    with keys masked out through the per-key bias."""
+    B, H, L, D = q.shape
+    scale = D**-0.5 if scale is None else scale
+    out_dtype = q.dtype
+    if q.dtype != torch.bfloat16:
+        q, k, v = q.to(torch.bfloat16), k.to(torch.bfloat16), v.to(torch.bfloat16)
+    kb = _additive(key_padding_mask, key_padding_mask_mode, (B, L)) if key_padding_mask is not None else None
+    ab = _additive(attn_mask, attn_mask_mode, (L, L)) if attn_mask is not None else None
+    rp = rpe.to(torch.float32).reshape(-1, L, L) if rpe is not None else None
+    Lp = -(-L // 128) * 128
+    if Lp != L:
+        padn = Lp - L
+        q, k, v = (torch.nn.functional.pad(t, (0, 0, 0, padn)) for t in (q, k, v))
+        kb = torch.nn.functional.pad(kb if kb is not None else q.new_zeros((B, L), dtype=torch.float32), (0, padn),
+                                     value=float("-inf"))
+        if ab is not None:
+            ab = torch.nn.functional.pad(ab, (0, padn, 0, padn))
+        if rp is not None:
+            rp = torch.nn.functional.pad(rp, (0, padn, 0, padn))
+        nb = layout.shape[1]
+        nbp = -(-Lp // blk)
+        if nbp > nb:  # padded query rows / keys get their own diagonal blocks (the keys are masked by kbias)
+            lay = torch.zeros(layout.shape[0], nbp, nbp, dtype=layout.dtype)
+            lay[:, :nb, :nb] = layout
+            for i in range(nb, nbp):
+                lay[:, i, i] = 1
+            layout = lay
+    kb, ab, rp = (None if t is None else t.contiguous() for t in (kb, ab, rp))
+    out = BlockSparseAttnFn.apply(q, k, v, layout, blk, scale, kb, ab, rp)
+    if Lp != L:
+        out = out[:, :, :L]
+    return out if out.dtype == out_dtype else out.to(out_dtype)

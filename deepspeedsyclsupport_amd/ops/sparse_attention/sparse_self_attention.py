@@ -1,11 +1,11 @@
 """Block-sparse self-attention (reference `ops/sparse_attention/sparse_self_attention.py`,
 `bert_sparse_self_attention.py`, `sparse_attention_utils.py`).
 
-bf16 device inputs without extra masks run the block-sparse gfx950 flash kernel (`block_sparse.py`: only the key
-tiles the layout touches are visited). Otherwise the block layout is expanded once per sequence length into a
-token-level additive mask (cached on device) and attention runs through the fused SDPA path with that mask; padding
-/ attention masks in 'add' or 'mul' mode and relative position embeddings are folded in. Layouts and API are the
-reference's.
+16-bit device inputs run the block-sparse gfx950 flash kernels (`block_sparse.py`: only the key tiles the layout
+touches are visited); key-padding masks, attention masks ('add' or 'mul' mode) and relative position embeddings are
+applied inside those kernels, as the reference's sparse softmax does. Host / fp32 inputs take a dense reference
+path: the block layout is expanded into a token-level additive mask and attention runs through SDPA. Layouts and
+API are the reference's.
 """
 import torch
 import torch.nn as nn
@@ -56,8 +56,13 @@ class SparseSelfAttention(nn.Module):
             raise TypeError("sparse attention supports fp16/bf16/fp32")
         from . import block_sparse
         blk = self.sparsity_config.block
-        if block_sparse.native_ok(query, key, value, blk, rpe, key_padding_mask, attn_mask):
-            return block_sparse.block_sparse_attention(query, key, value, self.get_layout(L), blk)
+        if block_sparse.native_ok(query, key, value, blk):
+            # masks and relative position embeddings are applied inside the gfx950 kernels
+            return block_sparse.block_sparse_attention(
+                query, key, value, self.get_layout(L), blk, rpe=rpe, key_padding_mask=key_padding_mask,
+                attn_mask=attn_mask, key_padding_mask_mode=self.key_padding_mask_mode,
+                attn_mask_mode=self.attn_mask_mode)
+        # host tensors / fp32: dense reference path
         bias = self._block_mask(L, query.device)[None]              # [1, H, L, L]
         if rpe is not None:
             bias = bias + rpe.float().view(-1, H, L, L) if rpe.dim() == 4 else bias + rpe.float()
