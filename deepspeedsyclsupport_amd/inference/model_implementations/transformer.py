@@ -262,8 +262,10 @@ class DSInferenceLayer(nn.Module):
         scale = spec.attn_scale or 1.0 / math.sqrt(D)
         window = spec.layer_windows[self.layer_idx] if spec.layer_windows else spec.sliding_window
         # ALiBi / windowed prompts and chunk continuations: ragged paged flash prefill over the cache
-        paged = n > 1 and D == 128 and qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16 \
-            and (not meta.prefill_from_zero or alibi is not None or bool(window))
+        # (head dims other than 128 always take it: the dense flash forward is a 128-wide kernel)
+        paged = n > 1 and D in PAGED_HEAD_DIMS and qkv.is_cuda and qkv.dtype == torch.bfloat16 \
+            and kc.dtype == torch.bfloat16 and (not meta.prefill_from_zero or alibi is not None or bool(window)
+                                                or D != 128)
         if qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16:
             # one fused HIP epilogue: split + RoPE(q, k) + scatter k/v into the paged cache
             from ...ops.native import hip_ops
@@ -496,14 +498,32 @@ def _cached_attention(q, kc, vc, meta, scale, alibi, window):
     return torch.stack(outs, 0)
 
 
+PAGED_HEAD_DIMS = (64, 80, 96, 128, 256)  # instantiations of the paged prefill / decode kernels
+_UNIFORM_TABLES = {}
+
+
+def _uniform_tables(B, n, device):
+    """(cu_q, work) of a uniform batch: every layer of every prefill with this (batch, length) shares one device
+    copy, so the per-call host table build and H2D copy are paid once."""
+    key = (B, n, str(device))
+    hit = _UNIFORM_TABLES.get(key)
+    if hit is None:
+        nqb = -(-n // 128)
+        seq = torch.arange(B, dtype=torch.int32).repeat_interleave(nqb)
+        qb = torch.arange(nqb, dtype=torch.int32).repeat(B)
+        if len(_UNIFORM_TABLES) > 256:
+            _UNIFORM_TABLES.clear()
+        hit = _UNIFORM_TABLES[key] = (torch.arange(0, (B + 1) * n, n, dtype=torch.int32).to(device),
+                                      torch.stack([seq, qb], 1).contiguous().to(device))
+    return hit
+
+
 def _paged_attention_uniform(q, kc, vc, meta, scale, alibi, window):
-    """Uniform batch (v1 engine): q [B, n, Hq, 128] at positions start..start+n-1 per sequence -> [B, n, Hq, 128]
+    """Uniform batch (v1 engine): q [B, n, Hq, D] at positions start..start+n-1 per sequence -> [B, n, Hq, D]
     through the ragged paged flash-prefill kernel (K/V of the new tokens are already in the cache)."""
     from ...ops.native import hip_ops
     B, n, Hq, D = q.shape
-    cu = torch.arange(0, (B + 1) * n, n, dtype=torch.int32, device=q.device)
-    work = torch.tensor([(b, qb) for b in range(B) for qb in range(-(-n // 128))], dtype=torch.int32).to(
-        q.device, non_blocking=True)
+    cu, work = _uniform_tables(B, n, q.device)
     o = hip_ops().paged_prefill(q.reshape(B * n, Hq, D).contiguous(), kc, vc, meta.block_tables, meta.start_pos, cu,
                                 work, alibi, window, scale)
     return o.view(B, n, Hq, D)
@@ -524,7 +544,7 @@ def _ragged_attention(q, kc, vc, meta, scale, alibi, window):
     nd, S = meta.n_decode, len(meta.start_host)
     fast = q.is_cuda and q.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16
     from ...ops.native import hip_ops
-    if fast and D == 128 and nd < S:
+    if fast and D in PAGED_HEAD_DIMS and nd < S:
         out = hip_ops().paged_prefill(q.contiguous(), kc, vc, meta.block_tables, meta.start_pos, meta.cu_q, meta.work,
                                       alibi, window, scale)
     else:
@@ -533,7 +553,7 @@ def _ragged_attention(q, kc, vc, meta, scale, alibi, window):
             a, b = meta.cu_host[i], meta.cu_host[i + 1]
             out[a:b] = _seq_cached_attention(q[a:b], kc, vc, meta, i, scale, alibi, window)
     if nd:
-        if fast and D in (64, 128, 256):
+        if fast and D in PAGED_HEAD_DIMS:
             out[:nd] = hip_ops().paged_decode(q[:nd].contiguous(), kc, vc, meta.block_tables[:nd], meta.seq_lens[:nd],
                                               meta.max_len, scale, alibi, window)
         else:
@@ -570,7 +590,7 @@ def _seq_cached_attention(q, kc, vc, meta, i, scale, alibi, window):
 
 
 def _decode_attention(q, kc, vc, meta, scale, alibi, window):
-    if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128, 256):
+    if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in PAGED_HEAD_DIMS:
         from ...ops.native import hip_ops
         return hip_ops().paged_decode(q, kc, vc, meta.block_tables, meta.seq_lens, meta.max_len, scale,
                                       alibi, window)

@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
     float* __restrict__ part_ml,         // [B, Hq, S, 2]
     bf16* __restrict__ out,              // [B, Hq, D]  (written directly when S == 1)
     int Hq, int Hk, int BS, int max_blocks, int chunk, float scale, int window) {
-  static_assert(D % 64 == 0 && D <= 256, "head dim");
+  static_assert(D % 16 == 0 && D >= 64 && D <= 256, "head dim");
   extern __shared__ __attribute__((aligned(16))) float sm[];  // scores [G][chunk] + reduction scratch
   const int b = blockIdx.x, kh = blockIdx.y, split = blockIdx.z, S = gridDim.z;
   const int G = Hq / Hk;
@@ -45,10 +45,14 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
   float* scores = sm;                       // [G][chunk]
   float* red = sm + MAXG * MAX_CHUNK;       // [THREADS/64 * MAXG * 2]
 
-  // ---- q of the G heads of this GQA group; LPR = D/8 lanes cover one row, 8 elements each
-  constexpr int LPR = D / 8;                // lanes per key row (16 for D=128)
-  constexpr int RPW = 64 / LPR;             // rows per wave instruction
-  const int sub = lane / LPR, li = lane % LPR;
+  // ---- q of the G heads of this GQA group; LPR lanes cover one row, 8 elements each. LPR is D/8 rounded up to a
+  // power of two (head dims 80 and 96 use 16 lanes per row): the surplus lanes carry a zero query, re-read the row's
+  // last chunk (a cache hit) and never write
+  constexpr int CPR = D / 8;                                   // 16-byte chunks per row
+  constexpr int LPR = CPR <= 8 ? 8 : (CPR <= 16 ? 16 : 32);    // lanes per key row (16 for D=128)
+  constexpr int RPW = 64 / LPR;                                // rows per wave instruction
+  const int sub = lane / LPR, li_raw = lane % LPR, li = li_raw < CPR ? li_raw : CPR - 1;
+  const float lane_on = li_raw < CPR ? 1.f : 0.f;
   float qv[MAXG][8];
   // unconditional loads (clamped head index): a guarded load would make the compiler wait on each one in turn
 #pragma unroll
@@ -56,7 +60,7 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
     const int gc = g < G ? g : G - 1;
     Vec8<bf16>::load(q + ((int64_t)b * Hq + kh * G + gc) * D + li * 8, qv[g]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) qv[g][j] *= scale;
+    for (int j = 0; j < 8; ++j) qv[g][j] *= scale * lane_on;
   }
   // ---- phase 1: scores for keys of this split (UNR key rows per lane-group in flight per iteration)
   constexpr int UNR = 4;
@@ -84,7 +88,7 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
           for (int j = 0; j < 8; ++j) s = fmaf(qv[g][j], kv[u][j], s);
 #pragma unroll
           for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-          if (li == 0) {
+          if (li_raw == 0) {
             if (alibi) s += alibi[kh * G + g] * (float)(t - (T - 1));
             if (t < tlo) s = -INFINITY;
             scores[g * MAX_CHUNK + (t - t0)] = s;
@@ -95,7 +99,7 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
   }
   // V rows do not depend on the scores: start the first P.V pass's loads before the softmax phases
   constexpr int ROWS = THREADS / LPR;
-  const int r = tid / LPR, c = tid % LPR;
+  const int r = tid / LPR, c_raw = tid % LPR, c = c_raw < CPR ? c_raw : CPR - 1;
   float vpre[8];
   if (t0 + r < t1) {
     const int blk = bt[(t0 + r) / BS], off = (t0 + r) % BS;
@@ -161,8 +165,10 @@ __global__ void __launch_bounds__(THREADS) paged_decode_kernel(
 #pragma unroll
   for (int g = 0; g < MAXG; ++g) {
     if (g >= G) break;  // block-uniform
+    if (c_raw < CPR) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) rb[r * D + c * 8 + j] = acc[g][j];
+      for (int j = 0; j < 8; ++j) rb[r * D + c * 8 + j] = acc[g][j];
+    }
     __syncthreads();
     for (int idx = tid; idx < D; idx += THREADS) {
       float s = 0.f;
@@ -240,7 +246,8 @@ __global__ void __launch_bounds__(256) qkv_rope_append_kernel(
   // cache slot = its position
   const int t = blockIdx.x, h = blockIdx.y * (blockDim.x / tph) + threadIdx.x / tph;
   const int b = seq_ids ? seq_ids[t] : t / n_new, j = seq_ids ? 0 : t % n_new;
-  if (h >= H3) return;
+  // (head dims whose half does not divide the block leave a few surplus threads at the end)
+  if (h >= H3 || (int)threadIdx.x / tph >= (int)blockDim.x / tph) return;
   const bf16* src = qkv + ((int64_t)t * H3 + h) * D;
   bf16* dst;
   bf16* extra = nullptr;
@@ -311,6 +318,8 @@ extern "C" int ds_paged_decode(const void* q, const void* kc, const void* vc, co
     DS_CHECK_LAUNCH();                                                                                              \
   }
   if (D == 64) { LAUNCH(64) }
+  else if (D == 80) { LAUNCH(80) }
+  else if (D == 96) { LAUNCH(96) }
   else if (D == 128) { LAUNCH(128) }
   else if (D == 256) { LAUNCH(256) }
   else return (int)hipErrorInvalidValue;

@@ -20,7 +20,7 @@ int ds_rms_fwd(const void*, const void*, const void*, void*, void*, float*, int6
 int ds_qkv_rope_append(const void*, const float*, const float*, const int*, void*, void*, void*, void*, void*,
                        const int*, const int*, const int*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ds_paged_prefill(const void*, const void*, const void*, void*, const int*, const int*, const int*, const int*, int,
-                     const float*, int, int, int, int, int, float, hipStream_t);
+                     const float*, int, int, int, int, int, int, float, hipStream_t);
 int ds_paged_decode(const void*, const void*, const void*, const int*, const int*, const float*, float*, float*, void*,
                     int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int ds_kv_append(const void*, const void*, void*, void*, const int*, const int*, int, int, int, int, int, int,
@@ -317,16 +317,19 @@ Tensor dequant_sh(Tensor qsh, Tensor ssh, int64_t N, int64_t gs) {
   return w;
 }
 
-// Ragged paged flash prefill (attn/paged_prefill.hip): q [T, Hq, 128] bf16, caches [blocks, Hk, BS, 128],
+// Ragged paged flash prefill (attn/paged_prefill.hip): q [T, Hq, D] bf16, caches [blocks, Hk, BS, D], D in {64, 80,
+// 96, 128, 256},
 // block_table [nseq, max_blocks], start [nseq], cu_q [nseq + 1], work [nwork, 2] int32 built by the caller from the
 // same lengths (every (sequence, 128-row block) with block * 128 < that sequence's new tokens).
 Tensor paged_prefill(Tensor q, Tensor kc, Tensor vc, Tensor block_table, Tensor start, Tensor cu_q, Tensor work,
                      OptT alibi, int64_t window, double scale) {
   need(q, "q"); need(kc, "k_cache"); need(vc, "v_cache"); need(block_table, "block_table"); need(start, "start");
   need(cu_q, "cu_q"); need(work, "work");
-  TORCH_CHECK(q.scalar_type() == at::kBFloat16 && kc.scalar_type() == at::kBFloat16 && q.dim() == 3 && q.size(2) == 128,
-              "paged_prefill: bf16 q [T, Hq, 128]");
-  TORCH_CHECK(kc.dim() == 4 && kc.size(3) == 128 && vc.sizes() == kc.sizes(), "paged_prefill: caches [NB, Hk, BS, 128]");
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 && kc.scalar_type() == at::kBFloat16 && q.dim() == 3,
+              "paged_prefill: bf16 q [T, Hq, D]");
+  const int D = (int)q.size(2);
+  TORCH_CHECK(D == 64 || D == 80 || D == 96 || D == 128 || D == 256, "paged_prefill: head dim 64/80/96/128/256");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(3) == D && vc.sizes() == kc.sizes(), "paged_prefill: caches [NB, Hk, BS, D]");
   TORCH_CHECK(block_table.scalar_type() == at::kInt && start.scalar_type() == at::kInt && cu_q.scalar_type() == at::kInt &&
               work.scalar_type() == at::kInt, "paged_prefill: int32 tables");
   const int64_t nseq = start.numel();
@@ -343,7 +346,7 @@ Tensor paged_prefill(Tensor q, Tensor kc, Tensor vc, Tensor block_table, Tensor 
   auto o = torch::empty_like(q);
   check(ds_paged_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), o.data_ptr(), block_table.data_ptr<int>(),
                          start.data_ptr<int>(), cu_q.data_ptr<int>(), work.data_ptr<int>(), (int)work.size(0), al, Hq,
-                         Hk, (int)kc.size(2), (int)block_table.size(1), (int)window, (float)scale, stream()),
+                         Hk, D, (int)kc.size(2), (int)block_table.size(1), (int)window, (float)scale, stream()),
         "paged_prefill");
   return o;
 }

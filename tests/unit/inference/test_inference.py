@@ -205,6 +205,31 @@ def test_injected_bf16_gpu(kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,H,D", [("gptj", 1024, 256), ("gpt_neox", 384, 96), ("phi", 320, 80), ("gpt2", 256, 64)])
+def test_head_dims_take_the_paged_kernels_gpu(kind, H, D, monkeypatch):
+    """GPT-J (head dim 256), GPT-NeoX-20B (96) and Phi (80) shapes: prompt and decode attention run in the paged HIP
+    kernels (reference `softmax_context` is head-size generic, `pt_binding.cpp:434-557`) — the per-sequence SDPA
+    paths must not be reached — and match the fp32 HF model."""
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd.inference.model_implementations import transformer as tr
+    for name in ("_cached_attention", "_prefill_attention", "_seq_cached_attention"):
+        monkeypatch.setattr(tr, name, lambda *a, _n=name, **k: pytest.fail(f"{_n} reached for head dim {D}"))
+    m = tiny(kind, H=H).eval()
+    assert H // 4 == D
+    ids = _ids(B=3, S=100)
+    with torch.no_grad():
+        ref = m(ids).logits.float()
+    eng = ds.init_inference(m, dtype=torch.bfloat16, replace_with_kernel_inject=True)
+    out = eng(ids.cuda()).logits.float().cpu()
+    assert (out - ref).abs().max().item() < 0.05 * ref.abs().max().item() + 0.02
+    g = eng.generate(ids.cuda(), max_new_tokens=8).cpu()
+    with torch.no_grad():
+        full = m(g[:, :-1]).logits[:, -1].float()
+    step_logits = eng(g[:, :-1].cuda()).logits[:, -1].float().cpu()
+    assert (step_logits - full).abs().max().item() < 0.05 * full.abs().max().item() + 0.02
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["llama", "mixtral"])
 def test_decode_graph_matches_eager_gpu(kind):
     """HIP-graph decode == eager decode. For Mixtral this also proves the MoE block is capturable: routing, expert

@@ -8,11 +8,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _case(lens, starts, Hq, Hk, BS, alibi, window, seed=0):
+def _case(lens, starts, Hq, Hk, BS, alibi, window, seed=0, D=128):
     from deepspeedsyclsupport_amd.inference.model_implementations.transformer import RaggedMeta, alibi_slopes
     from deepspeedsyclsupport_amd.ops.native import hip_ops
     g = torch.Generator(device="cuda").manual_seed(seed)
-    D = 128
     S = len(lens)
     need = [-(-(st + n) // BS) for st, n in zip(starts, lens)]
     nblocks = sum(need) + 3
@@ -66,3 +65,19 @@ def test_paged_prefill_alibi_window(window):
 
 def test_paged_prefill_long_prefix():
     _case([256, 17], [3000, 4095], 8, 1, 64, alibi=False, window=0, seed=3)
+
+
+@pytest.mark.parametrize("D", [64, 80, 96, 256])
+@pytest.mark.parametrize("alibi,window", [(False, 0), (True, 70)])
+def test_paged_prefill_head_dims(D, alibi, window):
+    """GPT-2 / Phi / GPT-NeoX-20B / GPT-J head sizes through the same kernel template."""
+    _case([37, 1, 200, 129, 64], [0, 100, 0, 70, 333], 8, 2, 64, alibi=alibi, window=window, seed=D, D=D)
+
+
+def test_uniform_tables_are_cached():
+    from deepspeedsyclsupport_amd.inference.model_implementations import transformer as tr
+    a = tr._uniform_tables(3, 300, torch.device("cuda"))
+    b = tr._uniform_tables(3, 300, torch.device("cuda"))
+    assert a[0] is b[0] and a[1] is b[1]
+    assert a[0].tolist() == [0, 300, 600, 900]
+    assert a[1].tolist() == [[s, q] for s in range(3) for q in range(3)]

@@ -270,7 +270,7 @@ def _paged_ref(q, kc, vc, bt, lens, scale, alibi=None, window=0):
     return out
 
 
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [64, 80, 96, 128, 256])
 @pytest.mark.parametrize("hq,hk", [(8, 8), (32, 8), (8, 1)])
 @pytest.mark.parametrize("lens", [[1, 7, 64], [300, 2049, 5000]])
 def test_paged_decode(D, hq, hk, lens):
