@@ -89,15 +89,21 @@ def alibi_slopes(n_heads):
 
 
 class QuantLinearWeight:
-    """Group-quantised weight (int8/int4). Symmetric int8 with K a multiple of 64 is kept pre-shuffled for the decode
-    MFMA stream (`ops/int8_gemv.py`); everything else is dequantised into a temporary right before its GEMM."""
+    """Group-quantised weight (int8/int4). Symmetric int8 with K a multiple of 64 and int4 with K a multiple of 128
+    are kept in MFMA operand order for the decode streams (`ops/int8_gemv.py`, `ops/int4_gemv.py`; `i8` holds either);
+    everything else is dequantised into a temporary right before its GEMM."""
 
     def __init__(self, w, bits=8, group_size=64):
+        from ...ops.int4_gemv import Int4Weight
         from ...ops.int8_gemv import Int8Weight
         from ...ops.quantizer import quantize
         self.shape = w.shape
         self.dtype = w.dtype
-        self.i8 = Int8Weight(w, group_size) if Int8Weight.supported(w, bits, group_size) else None
+        self.i8 = None
+        if Int8Weight.supported(w, bits, group_size):
+            self.i8 = Int8Weight(w, group_size)
+        elif Int4Weight.supported(w, bits, group_size):
+            self.i8 = Int4Weight(w, group_size)
         self.qt = None if self.i8 is not None else \
             quantize(w, group_size=min(group_size, w.numel()), bits=bits, symmetric=True)
 

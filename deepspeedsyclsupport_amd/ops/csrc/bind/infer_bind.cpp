@@ -33,6 +33,12 @@ int64_t ds_skinny_i8_mfma_ws_floats(int);
 void ds_skinny_i8_tune(int, int, int);
 int ds_dequant_sh(const int8_t*, const float*, void*, int, int, int, hipStream_t);
 int ds_skinny_i8(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
+int ds_skinny_i4_mfma_ok(int, int, int);
+int ds_skinny_i4_mfma(const void*, const int8_t*, const float*, const void*, void*, float*, int, int, int, int,
+                      hipStream_t);
+int64_t ds_skinny_i4_mfma_ws_floats(int);
+void ds_skinny_i4_tune(int, int);
+int ds_dequant_sh4(const int8_t*, const float*, void*, int, int, int, hipStream_t);
 int ds_quantize(const void*, int8_t*, float*, float*, int64_t, int, int, int, int, unsigned, int, hipStream_t);
 int ds_dequantize(const int8_t*, const float*, const float*, void*, int64_t, int, int, int, int, hipStream_t);
 int ds_dequant_reduce(const int8_t*, const float*, void*, int64_t, int, int, float, int, hipStream_t);
@@ -317,6 +323,49 @@ Tensor dequant_sh(Tensor qsh, Tensor ssh, int64_t N, int64_t gs) {
   return w;
 }
 
+bool skinny_i4_ok(int64_t M, int64_t K, int64_t gs) { return ds_skinny_i4_mfma_ok((int)M, (int)K, (int)gs) != 0; }
+
+// int4 MFMA stream over the packed layout (ops/int4_gemv.py: pack_int4_operands): x [M, K] bf16 (M <= 16),
+// q4 int8 bytes [ceil(N/16), K/128, 64, 16], s4 fp32 [ceil(N/16), K/gs, 16] -> y [M, N] bf16
+Tensor skinny_i4(Tensor x, Tensor q4, Tensor s4, OptT bias, int64_t N, int64_t gs) {
+  need(x, "x"); need(q4, "q4"); need(s4, "s4");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "skinny_i4: x must be bf16 [M, K]");
+  TORCH_CHECK(q4.scalar_type() == at::kChar && s4.scalar_type() == at::kFloat, "skinny_i4: packed int8 bytes, fp32 scales");
+  const int64_t M = x.size(0), K = x.size(1), NB = (N + 15) / 16;
+  TORCH_CHECK(ds_skinny_i4_mfma_ok((int)M, (int)K, (int)gs) != 0, "skinny_i4: unsupported shape (M ", M, ", K ", K,
+              ", gs ", gs, ")");
+  TORCH_CHECK(q4.numel() == NB * 16 * K / 2 && s4.numel() == NB * 16 * (K / gs), "skinny_i4: q4 / s4 size");
+  TORCH_CHECK(NB * K < ((int64_t)1 << 40) && N < ((int64_t)1 << 31) / 16, "skinny_i4: matrix too large");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(q4.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_i4: 16-B aligned x / q4");
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    need(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kBFloat16, "skinny_i4: bias bf16 [N]");
+    bp = bias->data_ptr();
+  }
+  auto y = torch::empty({M, N}, x.options());
+  auto& ws = i8_workspace(x, N);  // same fp32 scratch contract as the int8 stream (zero between calls)
+  TORCH_CHECK(ws.acc.numel() >= ds_skinny_i4_mfma_ws_floats((int)N), "skinny_i4: workspace");
+  check(ds_skinny_i4_mfma(x.data_ptr(), q4.data_ptr<int8_t>(), s4.data_ptr<float>(), bp, y.data_ptr(),
+                          ws.acc.data_ptr<float>(), (int)M, (int)N, (int)K, (int)gs, stream()),
+        "skinny_i4");
+  return y;
+}
+
+// packed int4 (ops/int4_gemv.py) -> row-major bf16 [N, K]
+Tensor dequant_sh4(Tensor q4, Tensor s4, int64_t N, int64_t gs) {
+  need(q4, "q4"); need(s4, "s4");
+  TORCH_CHECK(q4.scalar_type() == at::kChar && s4.scalar_type() == at::kFloat && q4.dim() == 4, "dequant_sh4: layout");
+  const int64_t K = q4.size(1) * 128;
+  TORCH_CHECK(q4.size(0) == (N + 15) / 16 && q4.size(2) == 64 && q4.size(3) == 16 &&
+                  s4.numel() == q4.size(0) * 16 * (K / gs), "dequant_sh4: sizes");
+  auto w = torch::empty({N, K}, q4.options().dtype(at::kBFloat16));
+  check(ds_dequant_sh4(q4.data_ptr<int8_t>(), s4.data_ptr<float>(), w.data_ptr(), (int)N, (int)K, (int)gs, stream()),
+        "dequant_sh4");
+  return w;
+}
+
 // Ragged paged flash prefill (attn/paged_prefill.hip): q [T, Hq, D] bf16, caches [blocks, Hk, BS, D], D in {64, 80,
 // 96, 128, 256},
 // block_table [nseq, max_blocks], start [nseq], cu_q [nseq + 1], work [nwork, 2] int32 built by the caller from the
@@ -362,6 +411,11 @@ void register_inference_ops(pybind11::module& m) {
         py::arg("gs"));
   m.def("skinny_i8_sh", &skinny_i8_sh, py::arg("x"), py::arg("qsh"), py::arg("ssh"), py::arg("bias"), py::arg("N"),
         py::arg("gs"));
+  m.def("skinny_i4_ok", &skinny_i4_ok);
+  m.def("skinny_i4", &skinny_i4, py::arg("x"), py::arg("q4"), py::arg("s4"), py::arg("bias"), py::arg("N"),
+        py::arg("gs"));
+  m.def("skinny_i4_tune", [](int64_t p, int64_t wpc) { ds_skinny_i4_tune((int)p, (int)wpc); });
+  m.def("dequant_sh4", &dequant_sh4);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_force_valu", &skinny_force_valu);
   m.def("skinny_set_path", &skinny_set_path);

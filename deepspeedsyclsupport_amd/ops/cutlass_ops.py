@@ -7,14 +7,16 @@ written into `output` — on the MI355X int8 kernels instead of CUTLASS:
  * int8: the per-channel weight is re-laid ONCE (cached per weight tensor) into the pre-shuffled MFMA operand layout
    of `csrc/gemv/skinny_int8.hip`; up to 16 token rows run the fused-dequant MFMA stream, larger batches dequantise
    straight from that layout (`dequant_sh`) into the library GEMM;
- * int4: unpacked to the same int8 layout at first use (the weight stream then costs int8 bytes; no native int4
-   kernel — recorded as such in `op_builder.InferenceCutlassBuilder`);
+ * int4: re-packed ONCE into the operand layout of `csrc/gemv/skinny_int4.hip` (K a multiple of 128): decode streams
+   half a byte per weight through the fused-dequant MFMA kernel, larger batches dequantise from that layout
+   (`dequant_sh4`) into the library GEMM;
  * MoE: per-expert weights [E, in, out] with expert-sorted token counts, each expert one of the above (or plain
    bf16 when unquantised) — the grouped-GEMM kernels of `ops/moe_ops.py` cover the unquantised MoE path.
 """
 import torch
 import torch.nn.functional as F
 
+from .int4_gemv import Int4Weight
 from .int8_gemv import Int8Weight, preshuffle
 from .transformer.functional import ACT_CODES
 from . import reference
@@ -72,7 +74,12 @@ class MixedGEMM:
         w = self._cache.get(key)
         if w is None:
             q = unpack_int4(weights) if self.num_bits == 4 else weights
-            if q.shape[0] % 64 == 0:
+            if self.num_bits == 4 and q.shape[0] % 128 == 0:
+                # per-output-channel scales = one scale group spanning K
+                K, N = q.shape
+                w = Int4Weight(q=q.t().contiguous(), scales=scales.float().reshape(-1).contiguous(), group_size=K,
+                               dtype=self.fp_dtype)
+            elif q.shape[0] % 64 == 0:
                 w = _PerChannel(q, scales, self.fp_dtype)
             else:  # K not a multiple of 64: keep the dequantised weight (no pre-shuffled layout possible)
                 w = (q.float() * scales.float().reshape(1, -1)).t().contiguous().to(self.fp_dtype)
@@ -83,7 +90,7 @@ class MixedGEMM:
         w = self._weight(weights, scales)
         x = hidden_states.to(self.fp_dtype)
         b = biases.to(self.fp_dtype) if biases is not None else None
-        y = w.linear(x, b) if isinstance(w, Int8Weight) else F.linear(x, w, b)
+        y = w.linear(x, b) if isinstance(w, (Int8Weight, Int4Weight)) else F.linear(x, w, b)
         if self.act != "identity":
             y = reference.ACTS[ACT_CODES[self.act]](y.float()).to(y.dtype)
         output.copy_(y.reshape(output.shape))

@@ -49,6 +49,7 @@ EXTENSIONS = {
             "gemv/skinny_gemm.hip",
             "gemv/skinny_mfma.hip",
             "gemv/skinny_int8.hip",
+            "gemv/skinny_int4.hip",
             "moe/moe_kernels.hip",
             "comm/xgmi_allreduce.hip",
         ],
@@ -305,14 +306,14 @@ class EvoformerAttnBuilder(OpBuilder):
 
 class InferenceCutlassBuilder(OpBuilder):
     """Reference `op_builder/inference_cutlass_builder.py` (CUTLASS `mixed_gemm` / `moe_gemm`): `load()` gives the
-    same entry points on the MI355X int8 kernels (`ops/cutlass_ops.py`). int8 weights run natively (pre-shuffled
-    MFMA stream / dequant + library GEMM); int4 weights are unpacked to int8 at first use — there is no native int4
-    kernel, so `is_compatible(num_bits=4)` says False."""
+    same entry points on the MI355X weight-only kernels (`ops/cutlass_ops.py`). int8 and int4 weights both run
+    natively: pre-shuffled / packed MFMA streams for decode (`csrc/gemv/skinny_int8.hip`, `skinny_int4.hip`) and a
+    dequantise-from-the-packed-layout + library GEMM for prefill. FP6 is not provided."""
     NAME = "cutlass_ops"
     EXT = "ds_hip_ops"
 
     def is_compatible(self, verbose=False, num_bits=8):
-        return num_bits == 8 and super().is_compatible(verbose)
+        return num_bits in (4, 8) and super().is_compatible(verbose)
 
     def load(self, verbose=False):
         import types

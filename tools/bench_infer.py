@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--gen", type=int, default=128)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--graph", default="0,1")
+    ap.add_argument("--quant-bits", type=int, default=0, help="weight-only quantisation of the layer GEMMs (8 or 4)")
+    ap.add_argument("--group-size", type=int, default=128)
     args = ap.parse_args()
     from deepspeedsyclsupport_amd.inference.config import DeepSpeedInferenceConfig
     from deepspeedsyclsupport_amd.inference.engine import InferenceEngine
@@ -36,6 +38,13 @@ def main():
         for p in model.parameters():
             if p.dim() >= 2:
                 p.normal_(0, 0.02)
+    bf16_bytes = sum(p.numel() * 2 for layer in model.layers for p in layer.parameters() if p.dim() >= 2)
+    stream_bytes = bf16_bytes
+    if args.quant_bits:
+        model.quantize_weights(args.quant_bits, args.group_size)
+        torch.cuda.empty_cache()
+        stream_bytes = sum(q.i8.nbytes() for layer in model.layers for q in layer.quant.values())
+    head_bytes = model.lm_head.numel() * 2
     for use_graph in [int(x) for x in args.graph.split(",")]:
         cfg = DeepSpeedInferenceConfig(dtype="bf16", enable_cuda_graph=bool(use_graph), max_tokens=4096)
         eng = InferenceEngine.__new__(InferenceEngine)
@@ -60,7 +69,15 @@ def main():
                               "hip_graph": bool(use_graph), "prefill_ms": round(t_prefill * 1e3, 2),
                               "prefill_tok_s": round(B * args.prompt / t_prefill, 1),
                               "decode_ms_per_token": round(dec * 1e3, 3),
-                              "decode_tok_s": round(B / dec, 1)}), flush=True)
+                              "decode_tok_s": round(B / dec, 1),
+                              "weight_bits": args.quant_bits or 16, "group_size": args.group_size,
+                              "layer_weight_gib_streamed": round(stream_bytes / 2**30, 3),
+                              "lm_head_gib_bf16": round(head_bytes / 2**30, 3),
+                              # bytes the decode step really reads (packed weights + scales + bf16 LM head) per second
+                              "weight_stream_tb_s": round((stream_bytes + head_bytes) / dec / 1e12, 2),
+                              # the same step priced at the bf16 model's bytes: what a bf16 decode would need to match
+                              "bf16_equivalent_tb_s": round((bf16_bytes + head_bytes) / dec / 1e12, 2)}),
+                  flush=True)
 
 
 if __name__ == "__main__":
