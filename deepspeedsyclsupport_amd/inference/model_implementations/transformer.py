@@ -118,6 +118,12 @@ def _weight(w):
     return w.materialize() if isinstance(w, QuantLinearWeight) else w
 
 
+def materialize(h):
+    """A layer of the weight-only decode path returns its output still in the GEMV workspace (`PendingAcc`); anything
+    other than the next such layer's input norm takes the plain tensor."""
+    return h.finalize() if hasattr(h, "finalize_rms") else h
+
+
 @dataclass
 class BatchMeta:
     block_tables: torch.Tensor       # [B, max_blocks] int32 (device)
@@ -404,8 +410,48 @@ class DSInferenceLayer(nn.Module):
                 down = down + self.fc2_b
         return down, res2
 
+    # ------------------------------------------------------------------------------ weight-only decode fast path
+    def _quant_skinny_ok(self, h):
+        spec = self.spec
+        if not self.quant or self.split_w or spec.norm != "rms" or spec.parallel_residual or spec.num_experts \
+                or self.tp != 1:
+            return False
+        from ...ops.int8_gemv import PendingAcc, raw_ok
+        if isinstance(h, PendingAcc):
+            return True
+        return raw_ok(h) and all(self.quant.get(n) is not None and self.quant[n].i8 is not None
+                                 for n in ("qkv_w", "o_w", "fc1_w", "fc2_w"))
+
+    def _forward_quant_skinny(self, h, residual, meta, cache, rope, alibi):
+        """Decode (<= 16 token rows) over int8 / int4 weights: the four weight streams leave their sums in the fp32
+        split-K workspace and the op that consumes each projection anyway — residual add + RMSNorm after the
+        attention-output and MLP-down projections, the gated activation after gate/up — converts and re-zeroes it
+        (`csrc/gemv/skinny_finalize.hip`). The block output is returned still pending: the next layer's input norm
+        consumes it. 8 launches per layer instead of 14."""
+        from ...ops.int8_gemv import PendingAcc
+        from ...ops.transformer.functional import ACT_CODES
+        eps, q = self.spec.norm_eps, self.quant
+        if isinstance(h, PendingAcc):
+            normed, res1 = h.finalize_rms(residual, self.ln1_w, eps)
+        elif residual is None:
+            normed, res1 = self._norm(h, self.ln1_w, None), h
+        else:
+            normed, res1 = self._norm(h, self.ln1_w, None, residual)
+        qkv = q["qkv_w"].i8.linear(normed, self.qkv_b)
+        attn = self._attend(qkv, meta, cache, rope, alibi)
+        normed2, res2 = q["o_w"].i8.raw(attn, self.o_b).finalize_rms(res1, self.ln2_w, eps)
+        up = q["fc1_w"].i8.raw(normed2, self.fc1_b)
+        if self.spec.gated_mlp:
+            mid = up.finalize_gated(ACT_CODES[self.spec.act])
+        else:
+            mid = DF.bias_activation(up.finalize(), None, self.spec.act)
+        return q["fc2_w"].i8.raw(mid, self.fc2_b), res2
+
     def forward(self, h, residual, meta, cache, rope, alibi):
         """Pre-norm block. Returns (block_output, residual) where the caller adds them (fused in the next norm)."""
+        if self._quant_skinny_ok(h):
+            return self._forward_quant_skinny(h, residual, meta, cache, rope, alibi)
+        h = materialize(h)
         if self._skinny_ok(h):
             return self._forward_skinny(h, residual, meta, cache, rope, alibi)
         if self.spec.parallel_residual:
@@ -683,6 +729,7 @@ class DSInferenceModel(nn.Module):
         rope = (self.rope_cos, self.rope_sin)
         for layer in self.layers:
             h, residual = layer(h, residual, meta, self.cache, rope, self.alibi)
+        h = materialize(h)
         if not all_logits:
             h = h[:, -1].contiguous()
             residual = residual[:, -1].contiguous() if residual is not None else None
@@ -711,6 +758,7 @@ class DSInferenceModel(nn.Module):
         rope = (self.rope_cos, self.rope_sin)
         for layer in self.layers:
             h, residual = layer(h, residual, meta, self.cache, rope, self.alibi)
+        h = materialize(h)
         h = h[0].index_select(0, meta.last_idx)
         residual = residual[0].index_select(0, meta.last_idx) if residual is not None else None
         if (h.is_cuda and h.dtype == torch.bfloat16 and self.spec.final_norm and self.spec.norm == "rms"

@@ -37,8 +37,11 @@ int ds_skinny_i4_mfma_ok(int, int, int);
 int ds_skinny_i4_mfma(const void*, const int8_t*, const float*, const void*, void*, float*, int, int, int, int,
                       hipStream_t);
 int64_t ds_skinny_i4_mfma_ws_floats(int);
-void ds_skinny_i4_tune(int, int);
+void ds_skinny_i4_tune(int, int, int);
 int ds_dequant_sh4(const int8_t*, const float*, void*, int, int, int, hipStream_t);
+int ds_skinny_finalize_rms(float*, const void*, const void*, const void*, void*, void*, int, int, int, float, hipStream_t);
+int ds_skinny_finalize_gated(float*, const void*, void*, int, int, int, int, hipStream_t);
+int ds_skinny_finalize_plain(float*, const void*, void*, int, int, int, hipStream_t);
 int ds_quantize(const void*, int8_t*, float*, float*, int64_t, int, int, int, int, unsigned, int, hipStream_t);
 int ds_dequantize(const int8_t*, const float*, const float*, void*, int64_t, int, int, int, int, hipStream_t);
 int ds_dequant_reduce(const int8_t*, const float*, void*, int64_t, int, int, float, int, hipStream_t);
@@ -353,6 +356,76 @@ Tensor skinny_i4(Tensor x, Tensor q4, Tensor s4, OptT bias, int64_t N, int64_t g
   return y;
 }
 
+// The int8 / int4 stream WITHOUT its finalize pass: returns the fp32 workspace view [16, NP] holding the sums of the M
+// token rows (no bias). The caller must hand it to one of the skinny_finalize* ops before the next weight-only GEMV on
+// this stream (they convert, fuse the consumer's element-wise work and re-zero the workspace).
+Tensor skinny_q_raw(Tensor x, Tensor wq, Tensor ws_s, int64_t N, int64_t gs, int64_t bits) {
+  need(x, "x"); need(wq, "wq"); need(ws_s, "scales");
+  TORCH_CHECK(bits == 4 || bits == 8, "skinny_q_raw: 4 or 8 bits");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "skinny_q_raw: x must be bf16 [M, K]");
+  TORCH_CHECK(wq.scalar_type() == at::kChar && ws_s.scalar_type() == at::kFloat, "skinny_q_raw: int8 bytes, fp32 scales");
+  const int64_t M = x.size(0), K = x.size(1), NB = (N + 15) / 16;
+  const bool ok = bits == 4 ? ds_skinny_i4_mfma_ok((int)M, (int)K, (int)gs) != 0 : ds_skinny_i8_mfma_ok((int)M, (int)K, (int)gs) != 0;
+  TORCH_CHECK(ok, "skinny_q_raw: unsupported shape (M ", M, ", K ", K, ", gs ", gs, ")");
+  TORCH_CHECK(wq.numel() == NB * 16 * K * bits / 8 && ws_s.numel() == NB * 16 * (K / gs), "skinny_q_raw: weight / scale size");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(wq.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_q_raw: 16-B aligned x / weights");
+  auto& ws = i8_workspace(x, N);
+  const int64_t NP = ds_skinny_i8_mfma_ws_floats((int)N) / 16;
+  TORCH_CHECK(NP == ds_skinny_i4_mfma_ws_floats((int)N) / 16, "workspace layouts differ");
+  if (bits == 4)
+    check(ds_skinny_i4_mfma(x.data_ptr(), wq.data_ptr<int8_t>(), ws_s.data_ptr<float>(), nullptr, nullptr,
+                            ws.acc.data_ptr<float>(), (int)M, (int)N, (int)K, (int)gs, stream()), "skinny_i4 (raw)");
+  else
+    check(ds_skinny_i8_mfma(x.data_ptr(), wq.data_ptr<int8_t>(), ws_s.data_ptr<float>(), nullptr, nullptr,
+                            ws.acc.data_ptr<float>(), (int)M, (int)N, (int)K, (int)gs, stream()), "skinny_i8 (raw)");
+  return ws.acc.narrow(0, 0, 16 * NP).view({16, NP});
+}
+
+const void* opt_bf16(const OptT& t, int64_t numel, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  need(*t, what);
+  TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->numel() == numel, what, ": bf16 with ", numel, " elements");
+  return t->data_ptr();
+}
+void check_acc(const Tensor& acc, int64_t M, int64_t N) {
+  TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat && acc.dim() == 2 && acc.size(0) == 16 &&
+                  acc.is_contiguous() && acc.size(1) >= N && M >= 1 && M <= 16, "skinny_finalize: fp32 workspace view [16, NP]");
+}
+
+// (acc + bias + residual) -> res_out; RMSNorm(res_out) * w -> y   (both [M, N] bf16)
+std::vector<Tensor> skinny_finalize_rms(Tensor acc, int64_t M, int64_t N, OptT bias, OptT residual, Tensor w, double eps) {
+  check_acc(acc, M, N);
+  const void* bp = opt_bf16(bias, N, "bias");
+  const void* rp = opt_bf16(residual, M * N, "residual");
+  OptT wo = w;
+  const void* wp = opt_bf16(wo, N, "norm weight");
+  auto y = torch::empty({M, N}, acc.options().dtype(at::kBFloat16));
+  auto res = torch::empty({M, N}, acc.options().dtype(at::kBFloat16));
+  check(ds_skinny_finalize_rms(acc.data_ptr<float>(), bp, rp, wp, y.data_ptr(), res.data_ptr(), (int)M, (int)N,
+                               (int)acc.size(1), (float)eps, stream()), "skinny_finalize_rms");
+  return {y, res};
+}
+
+// act(acc[:, :I] + b) * (acc[:, I:] + b) -> [M, N / 2] bf16
+Tensor skinny_finalize_gated(Tensor acc, int64_t M, int64_t N, OptT bias, int64_t act) {
+  check_acc(acc, M, N);
+  const void* bp = opt_bf16(bias, N, "bias");
+  auto out = torch::empty({M, N / 2}, acc.options().dtype(at::kBFloat16));
+  check(ds_skinny_finalize_gated(acc.data_ptr<float>(), bp, out.data_ptr(), (int)M, (int)N, (int)acc.size(1), (int)act,
+                                 stream()), "skinny_finalize_gated");
+  return out;
+}
+
+Tensor skinny_finalize(Tensor acc, int64_t M, int64_t N, OptT bias) {
+  check_acc(acc, M, N);
+  const void* bp = opt_bf16(bias, N, "bias");
+  auto y = torch::empty({M, N}, acc.options().dtype(at::kBFloat16));
+  check(ds_skinny_finalize_plain(acc.data_ptr<float>(), bp, y.data_ptr(), (int)M, (int)N, (int)acc.size(1), stream()),
+        "skinny_finalize");
+  return y;
+}
+
 // packed int4 (ops/int4_gemv.py) -> row-major bf16 [N, K]
 Tensor dequant_sh4(Tensor q4, Tensor s4, int64_t N, int64_t gs) {
   need(q4, "q4"); need(s4, "s4");
@@ -414,8 +487,13 @@ void register_inference_ops(pybind11::module& m) {
   m.def("skinny_i4_ok", &skinny_i4_ok);
   m.def("skinny_i4", &skinny_i4, py::arg("x"), py::arg("q4"), py::arg("s4"), py::arg("bias"), py::arg("N"),
         py::arg("gs"));
-  m.def("skinny_i4_tune", [](int64_t p, int64_t wpc) { ds_skinny_i4_tune((int)p, (int)wpc); });
+  m.def("skinny_i4_tune", [](int64_t p, int64_t wpc, int64_t rounds) { ds_skinny_i4_tune((int)p, (int)wpc, (int)rounds); },
+        py::arg("p"), py::arg("wpc"), py::arg("rounds") = 0);
   m.def("dequant_sh4", &dequant_sh4);
+  m.def("skinny_q_raw", &skinny_q_raw);
+  m.def("skinny_finalize_rms", &skinny_finalize_rms);
+  m.def("skinny_finalize_gated", &skinny_finalize_gated);
+  m.def("skinny_finalize", &skinny_finalize);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_force_valu", &skinny_force_valu);
   m.def("skinny_set_path", &skinny_set_path);

@@ -249,14 +249,16 @@ extern "C" int ds_dequant_sh4(const int8_t* Q4, const float* S4, void* W, int N,
 extern "C" int64_t ds_skinny_i4_mfma_ws_floats(int N) { return 16LL * (((N + 15) / 16 + 3) / 4) * 64; }
 
 // Variant override for tools/bench_int4_gemv.py (0 = default): in-flight quarters P and resident waves per CU.
-static int g_i4_p = 0, g_i4_wpc = 0;
-extern "C" void ds_skinny_i4_tune(int p, int wpc) {
+static int g_i4_p = 0, g_i4_wpc = 0, g_i4_rounds = 0;
+extern "C" void ds_skinny_i4_tune(int p, int wpc, int rounds) {
   g_i4_p = p;
   g_i4_wpc = wpc;
+  g_i4_rounds = rounds;
 }
 
 // X [M, K] bf16 (M <= 16), Q4 / S4 in the packed layout above (N padded to a multiple of 16), bias bf16 [N] or null
-// -> Y [M, N] bf16
+// -> Y [M, N] bf16. Y == null leaves the sums in the workspace (rows < M, row length ds_skinny_i4_mfma_ws_floats / 16)
+// for a fused consumer (skinny_finalize.hip), which then owes the re-zeroing.
 extern "C" int ds_skinny_i4_mfma(const void* X, const int8_t* Q4, const float* S4, const void* bias, void* Y, float* ws,
                                  int M, int N, int K, int gs, hipStream_t st) {
   if (!ds_skinny_i4_mfma_ok(M, K, gs) || N <= 0) return (int)hipErrorInvalidValue;
@@ -282,7 +284,8 @@ extern "C" int ds_skinny_i4_mfma(const void* X, const int8_t* Q4, const float* S
   const int P = g_i4_p ? g_i4_p : 2;
   const int wpc = g_i4_wpc ? g_i4_wpc : 12;
   // one resident round of waves, each with the same number of quarters (at least two rounds of the pipeline each)
-  const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(a.total / (2 * P), 256 * wpc));
+  const int rounds = g_i4_rounds ? g_i4_rounds : 2;
+  const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(a.total / (rounds * P), 256 * wpc));
   const dim3 grid((int)((waves + 3) / 4));
   const int spq = gs >= 128 ? 1 : 128 / gs;
 #define DS_I4_GO(PP, SS) hipLaunchKernelGGL((skinny_i4_mfma_kernel<FB, PP, SS>), grid, dim3(256), 0, st, a)
@@ -293,6 +296,7 @@ extern "C" int ds_skinny_i4_mfma(const void* X, const int8_t* Q4, const float* S
   }
 #undef DS_I4_GO
   DS_CHECK_LAUNCH();
+  if (Y == nullptr) return 0;
   hipLaunchKernelGGL(skinny_i4_finalize, dim3((int)(((int64_t)M * a.NP + 255) / 256)), dim3(256), 0, st, ws,
                      (const bf16*)bias, (bf16*)Y, M, N, a.NP);
   DS_CHECK_LAUNCH();

@@ -353,7 +353,7 @@ extern "C" int ds_skinny_i8_mfma_ok(int M, int K, int gs) {
 extern "C" int64_t ds_skinny_i8_mfma_ws_floats(int N) { return 16LL * (((N + 15) / 16 + 3) / 4) * 64; }
 
 // X [M, K] bf16 (M <= 16), Qsh / Ssh in the shuffled layout above (N padded to a multiple of 16), bias bf16 [N] or
-// null -> Y [M, N] bf16
+// null -> Y [M, N] bf16 (Y == null: leave the sums in the workspace, row length ws_floats / 16, un-finalized)
 extern "C" int ds_skinny_i8_mfma(const void* X, const int8_t* Qsh, const float* Ssh, const void* bias, void* Y,
                                  float* ws, int M, int N, int K, int gs, hipStream_t st) {
   if (!ds_skinny_i8_mfma_ok(M, K, gs) || N <= 0) return (int)hipErrorInvalidValue;
@@ -380,6 +380,7 @@ extern "C" int ds_skinny_i8_mfma(const void* X, const int8_t* Qsh, const float* 
     a.total = (int64_t)nbg * a.KQ;
     const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(a.total / (2 * P), 256 * wpc));
     hipLaunchKernelGGL(kern, dim3((int)((waves + 3) / 4)), dim3(256), 0, st, a);
+    if (Y == nullptr) return;  // sums stay in the workspace for a fused consumer (skinny_finalize.hip)
     hipLaunchKernelGGL(skinny_i8_finalize, dim3((int)(((int64_t)M * a.NP + 255) / 256)), dim3(256), 0, st, ws,
                        (const bf16*)bias, (bf16*)Y, M, N, a.NP);
   };

@@ -19,6 +19,7 @@ the library GEMM.
 import torch
 import torch.nn.functional as F
 
+from .int8_gemv import PendingAcc
 from .native import hip_ops
 from .quantizer import quantize
 
@@ -103,6 +104,13 @@ class Int4Weight:
         K = self.shape[1]
         return (q.float().reshape(self.shape[0], K // self.group_size, self.group_size) *
                 s.reshape(self.shape[0], -1, 1)).reshape(self.shape[0], K).to(dtype)
+
+    def raw(self, x, bias=None):
+        """Decode GEMV without its finalize pass (see `int8_gemv.PendingAcc`); `int8_gemv.raw_ok` must hold."""
+        K = x.shape[-1]
+        acc = hip_ops().skinny_q_raw(x.reshape(-1, K).contiguous(), self.q4, self.s4, self.shape[0], self.group_size,
+                                     4)
+        return PendingAcc(acc, x.shape[:-1], self.shape[0], bias)
 
     def linear(self, x, bias=None):
         """x [..., K] -> x . W^T (+ bias). Up to 16 token rows on a GPU: the fused MFMA stream over the packed weight;

@@ -25,6 +25,45 @@ from .quantizer import QuantizedTensor, dequantize, quantize
 MAX_DECODE_ROWS = 16
 
 
+class PendingAcc:
+    """A decode GEMV whose fp32 sums still sit in the stream's split-K workspace (no bias applied yet). Exactly one
+    of the `finalize*` methods must run before the next weight-only GEMV on the stream: each converts the sums,
+    fuses the element-wise op that consumes the projection anyway, and re-zeroes the workspace — one kernel instead
+    of finalize + consumer (`csrc/gemv/skinny_finalize.hip`)."""
+
+    def __init__(self, acc, lead_shape, N, bias=None):
+        self.acc, self.lead, self.N, self.bias = acc, tuple(lead_shape), N, bias
+        self.M = 1
+        for d in self.lead:
+            self.M *= d
+        self.done = False
+
+    def _take(self):
+        if self.done:
+            raise RuntimeError("the workspace of this GEMV was already consumed")
+        self.done = True
+        return self.acc
+
+    def finalize(self):
+        return hip_ops().skinny_finalize(self._take(), self.M, self.N, self.bias).view(*self.lead, self.N)
+
+    def finalize_rms(self, residual, weight, eps):
+        """-> (RMSNorm(sums + bias + residual) * weight, sums + bias + residual)"""
+        r = None if residual is None else residual.reshape(self.M, self.N).contiguous()
+        y, res = hip_ops().skinny_finalize_rms(self._take(), self.M, self.N, self.bias, r, weight, eps)
+        return y.view(*self.lead, self.N), res.view(*self.lead, self.N)
+
+    def finalize_gated(self, act_code):
+        """-> act(gate + b) * (up + b) for a fused [gate | up] projection"""
+        return hip_ops().skinny_finalize_gated(self._take(), self.M, self.N, self.bias, act_code).view(
+            *self.lead, self.N // 2)
+
+
+def raw_ok(x, bias=None):
+    return x.is_cuda and x.dtype == torch.bfloat16 and x.numel() // x.shape[-1] <= MAX_DECODE_ROWS and \
+        (bias is None or bias.dtype == torch.bfloat16)
+
+
 def preshuffle(q, scales, group_size):
     """Row-major int8 q [N, K] + fp32 scales [N * K / gs] -> (qsh [NB, K/64, 64, 16], ssh [NB, K/gs, 16]), N padded
     to NB * 16 rows with zero weights / zero scales."""
@@ -76,6 +115,13 @@ class Int8Weight:
         qt = QuantizedTensor(q.reshape(-1), s, torch.empty(0, device=q.device), self.shape, self.group_size, 8,
                              self.dtype)
         return dequantize(qt, dtype)
+
+    def raw(self, x, bias=None):
+        """Decode GEMV without its finalize pass (see `PendingAcc`); `raw_ok(x, bias)` must hold."""
+        K = x.shape[-1]
+        acc = hip_ops().skinny_q_raw(x.reshape(-1, K).contiguous(), self.qsh, self.ssh, self.shape[0],
+                                     self.group_size, 8)
+        return PendingAcc(acc, x.shape[:-1], self.shape[0], bias)
 
     def linear(self, x, bias=None):
         """x [..., K] -> x . W^T (+ bias). Up to 16 token rows on a GPU: the fused MFMA stream (no bf16 weight is

@@ -140,3 +140,47 @@ def test_int4_decode_follows_bf16_engine():
     l4 = e4(g16[:, :-1]).logits[:, -1].float()
     assert (l4 - l16).abs().max().item() < 0.35 * l16.abs().max().item() + 0.1
     assert e4.generate(ids, max_new_tokens=6).shape == g16.shape
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 512), (5, 1000, 256), (16, 14336, 256), (3, 72, 128)])
+def test_fused_finalize_consumers(bits, M, N, K):
+    """The stream without its finalize pass + (residual add + RMSNorm | gated activation | plain) consumers equal
+    the finalized GEMV followed by the separate ops, and leave the workspace zero for the next call."""
+    from deepspeedsyclsupport_amd.ops import reference
+    from deepspeedsyclsupport_amd.ops.int8_gemv import Int8Weight
+    from deepspeedsyclsupport_amd.ops.transformer.functional import ACT_CODES
+    torch.manual_seed(bits + M)
+    w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    W = i4.Int4Weight(w, 128) if bits == 4 else Int8Weight(w, 64)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, device="cuda").bfloat16()
+    res = torch.randn(M, N, device="cuda").bfloat16()
+    lnw = (1 + 0.1 * torch.randn(N, device="cuda")).bfloat16()
+    y = W.linear(x).float()                       # no bias: the workspace sums
+    # plain
+    torch.testing.assert_close(W.raw(x, b).finalize().float(), (y + b.float()).bfloat16().float(), rtol=1e-2, atol=1e-2)
+    # residual + RMSNorm
+    out, new_res = W.raw(x, b).finalize_rms(res, lnw, 1e-5)
+    r_ref = (y + b.float() + res.float()).bfloat16()
+    torch.testing.assert_close(new_res.float(), r_ref.float(), rtol=1e-2, atol=2e-2)
+    rf = new_res.float()
+    n_ref = rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + 1e-5) * lnw.float()
+    torch.testing.assert_close(out.float(), n_ref, rtol=2e-2, atol=2e-2)
+    out2, _ = W.raw(x).finalize_rms(None, lnw, 1e-5)  # no bias, no residual
+    n2 = y * torch.rsqrt(y.bfloat16().float().pow(2).mean(-1, keepdim=True) + 1e-5) * lnw.float()
+    torch.testing.assert_close(out2.float(), n2, rtol=2e-2, atol=2e-2)
+    # gated activation
+    if N % 2 == 0:
+        for act in ("silu", "gelu"):
+            g = W.raw(x, b).finalize_gated(ACT_CODES[act])
+            yy = y + b.float()
+            ref = reference.ACTS[ACT_CODES[act]](yy[:, :N // 2]) * yy[:, N // 2:]
+            torch.testing.assert_close(g.float(), ref, rtol=2e-2, atol=2e-2)
+    # the workspace is zero again: a plain call still matches
+    torch.testing.assert_close(W.linear(x).float(), y, rtol=0, atol=0)
+    p = W.raw(x)
+    p.finalize()
+    with pytest.raises(RuntimeError):
+        p.finalize()

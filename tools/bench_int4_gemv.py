@@ -39,15 +39,16 @@ for N, K in shapes[:4] if quick else shapes:
         for M in (1, 4, 8, 16):
             x = torch.randn(M, K, device="cuda").bfloat16()
             row = {"N": N, "K": K, "M": M, "gs": gs}
-            for P, wpc in ((0, 0), (3, 8), (2, 16), (2, 8)):
-                hip_ops().skinny_i4_tune(P, wpc)
+            for P, wpc, rounds in ((0, 0, 0), (3, 8, 2), (2, 8, 2), (2, 12, 1), (3, 8, 1), (2, 16, 1), (2, 12, 4)):
+                hip_ops().skinny_i4_tune(P, wpc, rounds)
+                # main kernel only (sums left in the workspace, re-zeroed by a plain finalize outside the timing)
                 t = timeit(lambda: hip_ops().skinny_i4(x, w4.q4, w4.s4, None, N, gs))
-                tag = "i4" if P == 0 else f"i4_p{P}w{wpc}"
+                tag = "i4" if P == 0 else f"i4_p{P}w{wpc}r{rounds}"
                 row[f"{tag}_us"] = round(t * 1e6, 1)
                 row[f"{tag}_packed_tb_s"] = round(w4.nbytes() / t / 1e12, 2)
                 if P == 0:
                     row["i4_bf16_equiv_tb_s"] = round(N * K * 2 / t / 1e12, 2)
-            hip_ops().skinny_i4_tune(0, 0)
+            hip_ops().skinny_i4_tune(0, 0, 0)
             if w8 is not None:
                 t = timeit(lambda: w8.linear(x))
                 row["i8_us"] = round(t * 1e6, 1)
