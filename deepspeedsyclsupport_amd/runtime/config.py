@@ -137,6 +137,9 @@ class AIOConfig(DeepSpeedConfigModel):
 class CheckpointConfig(DeepSpeedConfigModel):
     tag_validation: str = "Warn"
     load_universal: bool = False
+    # also write the optimizer state in the reference's own layout under <save_dir>/reference_format/<tag>
+    # (`checkpoint/reference_format.py`), for tools written against the reference's files
+    write_reference_format: bool = False
     use_node_local_storage: bool = False
     parallel_write: dict = {}
 

@@ -710,11 +710,32 @@ class DeepSpeedEngine(nn.Module):
         return None
 
     def _param_shapes(self):
+        """One ordered name -> full shape dict per optimizer param group, parameters in the group's own order
+        (reference `_get_zero_param_shapes`, `runtime/engine.py:3365-3400`: the order its ZeRO flattening uses)."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        opt = self.optimizer
+        if opt is not None and hasattr(opt, "param_to_og") and hasattr(opt, "opt_params"):
+            groups = [OrderedDict() for _ in range(opt.num_og)]
+            for p in opt.opt_params:
+                if id(p) in names:
+                    groups[opt.param_to_og[id(p)]][names[id(p)]] = torch.Size(getattr(p, "ds_shape", p.shape))
+            return groups
         shapes = OrderedDict()
         for n, p in self.module.named_parameters():
             if p.requires_grad:
                 shapes[n] = torch.Size(getattr(p, "ds_shape", p.shape))
         return [shapes]
+
+    def _shared_params(self):
+        """{alias name: canonical name} of tied parameters (reference `_get_shared_params`,
+        `runtime/engine.py:3402-3430`): consolidation tools re-create the aliases from it."""
+        first, shared = {}, {}
+        for n, p in self.module.named_parameters(remove_duplicate=False):
+            if id(p) in first:
+                shared[n] = first[id(p)]
+            else:
+                first[id(p)] = n
+        return shared
 
     def _checkpoint_tag_validation(self, tag):
         if not self._config.checkpoint_tag_validation_enabled or dist.get_world_size() == 1:
@@ -805,7 +826,7 @@ class DeepSpeedEngine(nn.Module):
                      optimizer=None,
                      param_shapes=self._param_shapes() if zero else None,
                      frozen_param_shapes=None,
-                     shared_params=None,
+                     shared_params=self._shared_params(),
                      frozen_param_fragments=None,
                      lr_scheduler=self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,
                      data_sampler=sampler,
@@ -830,11 +851,22 @@ class DeepSpeedEngine(nn.Module):
                 self._copy_recovery_script(save_dir)
         self.checkpoint_engine.commit(tag)
         dist.barrier()
+        if zero and getattr(self._config.checkpoint_config, "write_reference_format", False):
+            self._write_reference_format(save_dir, tag)
         if save_latest and dist.get_rank() == 0:
             with open(os.path.join(save_dir, "latest"), "w") as f:
                 f.write(tag)
         dist.barrier()
         return True
+
+    def _write_reference_format(self, save_dir, tag):
+        """Every data-parallel rank re-slices the (complete, just committed) native shards into the file the
+        reference would have written for it — no collective, one parameter in host memory at a time."""
+        from ..checkpoint import reference_format as rf
+        mp_rank = 0 if self.mpu is None else self.mpu.get_model_parallel_rank()
+        rf.export_rank(save_dir, tag, dist.get_rank(self.seq_data_parallel_group),
+                       dist.get_world_size(self.seq_data_parallel_group), mp_rank)
+        dist.barrier()
 
     def _copy_recovery_script(self, save_path):
         import shutil
@@ -879,8 +911,10 @@ class DeepSpeedEngine(nn.Module):
         need_shards = self.optimizer is not None and (not load_module_only or self._zero3_partitioned() or
                                                       bool(placeholders))
         if universal and need_shards:
-            from ..checkpoint.ds_to_universal import load_universal_into
-            load_universal_into(self.optimizer, self.module, tag_dir)
+            from ..checkpoint.universal_checkpoint import load_universal_into
+            tp_rank = 0 if self.mpu is None else self.mpu.get_model_parallel_rank()
+            tp_size = 1 if self.mpu is None else self.mpu.get_model_parallel_world_size()
+            load_universal_into(self.optimizer, self.module, tag_dir, tp_rank, tp_size)
         elif need_shards:
             with_states = load_optimizer_states and not load_module_only
             zpath = self._get_zero_ckpt_name(load_dir, tag)
@@ -928,13 +962,16 @@ class DeepSpeedEngine(nn.Module):
         if self.zero_optimization_partition_weights() and self.optimizer is not None:
             own = dict(self.module.named_parameters())
             placeholders, bad = [], []
+            wrote = False
             for n, v in sd.items():
                 p = own.get(n)
                 if p is None or not torch.is_tensor(v):
                     continue
                 want = getattr(p, "ds_numel", p.numel())
                 if v.numel() == want and v.numel() > 0:
-                    self.optimizer.set_full_fp32_param(p, v.to(self.device))
+                    # local copy into this rank's partition; the full buffers are refreshed once below
+                    self.optimizer._scatter_param(p, v, "fp32", also_shard=True)
+                    wrote = True
                 elif v.numel() == 0 and want > 0:
                     placeholders.append(n)
                 else:
@@ -945,6 +982,8 @@ class DeepSpeedEngine(nn.Module):
                 missing = [n for n in own if n not in sd]
                 if missing:
                     raise RuntimeError(f"missing keys in checkpoint module state: {missing[:5]}")
+            if wrote:
+                self.optimizer._post_step_gather()
             bufs = dict(self.module.named_buffers())
             for n, v in sd.items():
                 if n in bufs:

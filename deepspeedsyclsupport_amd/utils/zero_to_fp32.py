@@ -16,6 +16,9 @@ model-parallel ranks (one rank's files at a time) come out right. Files are read
 Format note: the flat-group shards are NOT the reference's per-group layout (`single_partition_of_fp32_groups`
 sliced by `param_shapes`), so the reference's zero_to_fp32 cannot read them; this script can, and
 `checkpoint/zero_checkpoint.py` reads both formats (the engine loads reference-format checkpoints through it).
+`"checkpoint": {"write_reference_format": true}` (or `python -m deepspeedsyclsupport_amd.checkpoint.reference_format`
+offline) additionally writes the reference's own layout under `<save_dir>/reference_format/<tag>` for tools written
+against it.
 """
 import argparse
 import glob

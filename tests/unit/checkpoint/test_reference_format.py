@@ -1,172 +1,174 @@
-"""Loading reference-layout ZeRO checkpoints.
+"""Reference-layout optimizer shards written next to the native ones (`checkpoint/reference_format.py`).
 
-No checkpoint produced by the reference ships in `/root/reference`, so these tests synthesise shard files exactly as
-the reference's save code lays them out — ZeRO-1/2: `stage_1_and_2.py:2102-2146` (`single_partition_of_fp32_groups`
-per optimizer group = the rank's slice of the group's flat tensor, flattened in `param_shapes` order and padded to a
-multiple of 2*dp; `base_optimizer_state` = the torch optimizer state of those flat partitions; a pickled
-`LossScaler` object), ZeRO-3: `stage3.py:2382-2395` (`fp32_flat_groups`, every parameter cut into
-ceil(numel / dp) pieces) — and check that the engine restores every fp32 master and Adam moment from them at the
-same and at a different data-parallel size. Byte parity with real reference files remains unpinned.
+The reader in this file is a test-side re-implementation of the reference's consolidation rules
+(`utils/zero_to_fp32.py:141-191` parse_optim_states, `:256-326` ZeRO-2 merge, `:350-444` ZeRO-3 merge) and of its
+universal-checkpoint fragment walk (`checkpoint/ds_to_universal.py:87-121`: `param_slice_mappings` start / numel into
+`single_partition_of_fp32_groups` and `base_optimizer_state`). It must rebuild every fp32 weight and Adam moment from
+the files this framework writes. No file written by the reference itself ships with it: byte parity stays unpinned.
 """
+import glob
 import math
 import os
-from collections import OrderedDict
+import re
 
 import pytest
 import torch
-
-from deepspeedsyclsupport_amd.checkpoint import zero_checkpoint as zc
 
 from ..common import run_distributed
 from ..simple_model import base_config, random_tokens, tiny_llama
 
 
-def _ref_values(seed=0):
-    model = tiny_llama(seed=seed)
-    g = torch.Generator().manual_seed(123)
-    vals = OrderedDict()
-    for n, p in model.named_parameters():
-        vals[n] = (p.detach().float().clone(), torch.randn(p.shape, generator=g) * 1e-3,
-                   torch.rand(p.shape, generator=g) * 1e-6)
-    return vals
-
-
-def _loss_scaler_obj():
-    stubs = zc._reference_pickle_stubs()
-    cls = [c for c in stubs if c.__name__ == "LossScaler"][0]
-    obj = cls.__new__(cls)
-    obj.__dict__.update({"cur_scale": 1.0, "dynamic": False})
-    return obj
-
-
-class _fake_reference_modules:
-    """Make the stub classes importable under the reference's module paths while the synthetic files are pickled
-    (the pickler checks importability); removed afterwards."""
-
-    def __enter__(self):
-        import sys
-        import types
-        self.added = []
-        for cls in zc._reference_pickle_stubs():
-            parts = cls.__module__.split(".")
-            for i in range(1, len(parts) + 1):
-                name = ".".join(parts[:i])
-                if name not in sys.modules:
-                    sys.modules[name] = types.ModuleType(name)
-                    self.added.append(name)
-            setattr(sys.modules[cls.__module__], cls.__qualname__, cls)
-        return self
-
-    def __exit__(self, *a):
-        import sys
-        for name in self.added:
-            sys.modules.pop(name, None)
-
-
-def write_reference_zero2(d, vals, world, step=3):
-    with _fake_reference_modules():
-        _write_reference_zero2(d, vals, world, step)
-
-
-def write_reference_zero3(d, vals, world, step=3):
-    with _fake_reference_modules():
-        _write_reference_zero3(d, vals, world, step)
-
-
-def _write_reference_zero2(d, vals, world, step=3):
-    os.makedirs(d, exist_ok=True)
-    names = list(vals.keys())
-    shapes = OrderedDict((n, vals[n][0].shape) for n in names)
-    torch.save({"module": {n: vals[n][0].bfloat16() for n in names}, "param_shapes": [shapes],
-                "global_steps": step, "dp_world_size": world}, os.path.join(d, "mp_rank_00_model_states.pt"))
-    flats = [torch.cat([vals[n][i].reshape(-1) for n in names]) for i in range(3)]
-    align = 2 * world
-    pad = (-flats[0].numel()) % align
-    flats = [torch.nn.functional.pad(f, (0, pad)) for f in flats]
-    P = flats[0].numel() // world
-    for r in range(world):
-        part = [f[r * P:(r + 1) * P].clone() for f in flats]
-        trimmed = part[0][:P - pad] if r == world - 1 else part[0]
-        osd = {
-            "loss_scaler": _loss_scaler_obj(), "dynamic_loss_scale": False, "overflow": False, "clip_grad": 1.0,
-            "base_optimizer_state": {"state": {0: {"step": torch.tensor(float(step)), "exp_avg": part[1],
-                                                   "exp_avg_sq": part[2]}},
-                                     "param_groups": [{"lr": 1e-2, "betas": (0.9, 0.999), "eps": 1e-8,
-                                                       "weight_decay": 0.01, "params": [0]}]},
-            "single_partition_of_fp32_groups": [trimmed], "zero_stage": 2, "group_paddings": [pad if r == world - 1
-                                                                                               else 0],
-            "partition_count": world, "ds_version": "0.12.7", "param_slice_mappings": [OrderedDict()],
-        }
-        torch.save({"optimizer_state_dict": osd}, os.path.join(d, f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"))
-
-
-def _write_reference_zero3(d, vals, world, step=3):
-    os.makedirs(d, exist_ok=True)
-    names = list(vals.keys())
-    shapes = OrderedDict((n, vals[n][0].shape) for n in names)
-    for r in range(world):
-        pieces = [[], [], []]
-        for n in names:
-            numel = vals[n][0].numel()
-            pn = math.ceil(numel / world)
-            for i in range(3):
-                flat = torch.nn.functional.pad(vals[n][i].reshape(-1), (0, pn * world - numel))
-                pieces[i].append(flat[r * pn:(r + 1) * pn])
-        fl = [torch.cat(x) for x in pieces]
-        torch.save({"module": {n: torch.empty(0, dtype=torch.bfloat16) for n in names}, "param_shapes": [shapes],
-                    "global_steps": step, "dp_world_size": world},
-                   os.path.join(d, f"zero_pp_rank_{r}_mp_rank_00_model_states.pt"))
-        osd = {"zero_stage": 3, "loss_scaler": _loss_scaler_obj(), "dynamic_loss_scale": False, "overflow": False,
-               "partition_count": world,
-               "optimizer_state_dict": {"state": {0: {"step": torch.tensor(float(step)), "exp_avg": fl[1],
-                                                      "exp_avg_sq": fl[2]}},
-                                        "param_groups": [{"lr": 1e-2, "params": [0]}]},
-               "fp32_flat_groups": [fl[0]]}
-        torch.save({"optimizer_state_dict": osd}, os.path.join(d, f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"))
-
-
-@pytest.mark.parametrize("stage", [2, 3])
-def test_sources_reconstruct_parameters(stage, tmp_path):
-    vals = _ref_values()
-    d = str(tmp_path / "t")
-    (write_reference_zero2 if stage == 2 else write_reference_zero3)(d, vals, 3)
-    src = zc.open_source(d)
-    assert isinstance(src, zc.ReferenceZero12Source if stage == 2 else zc.ReferenceZero3Source)
-    assert src.step() == 3
-    for n, (w, m, v) in vals.items():
-        torch.testing.assert_close(src.get(n, "fp32"), w, rtol=0, atol=0)
-        torch.testing.assert_close(src.get(n, "exp_avg"), m, rtol=0, atol=0)
-        torch.testing.assert_close(src.get(n, "exp_avg_sq"), v, rtol=0, atol=0)
-
-
-def _load_ref(stage, ckpt, tag, vals_path):
-    import sys
+def _train_and_save(stage, save_dir, out):
     import deepspeedsyclsupport_amd as ds
-    assert "deepspeed" not in sys.modules
+    from deepspeedsyclsupport_amd import comm as dist
     from deepspeedsyclsupport_amd.utils import safe_get_full_fp32_param, safe_get_full_optimizer_state
-    vals = torch.load(vals_path, weights_only=True)
-    c = base_config(stage=stage, lr=1e-2, dtype="fp32")
-    c["zero_optimization"].update({"reduce_bucket_size": 3000, "stage3_param_persistence_threshold": 100})
-    eng, _, _, _ = ds.initialize(model=tiny_llama(seed=9), config=c)
-    eng.load_checkpoint(ckpt, tag=tag)
-    assert eng.global_steps == 3
+    cfg = base_config(stage=stage, lr=1e-2, mb=2)
+    cfg["checkpoint"] = {"write_reference_format": True}
+    model = tiny_llama()
+    decay = [p for n, p in model.named_parameters() if p.dim() >= 2]
+    no_decay = [p for n, p in model.named_parameters() if p.dim() < 2]
+    groups = [{"params": decay, "weight_decay": 0.1}, {"params": no_decay, "weight_decay": 0.0}]
+    eng, _, _, _ = ds.initialize(model=model, model_parameters=groups, config=cfg)
+    for x in random_tokens(2, 2, 16, seed=5 + dist.get_rank()):
+        eng.backward(eng(x, labels=x))
+        eng.step()
+    eng.save_checkpoint(save_dir, tag="t")
+    full = {}
     for n, p in eng.module.named_parameters():
-        w, m, v = vals[n]
-        torch.testing.assert_close(safe_get_full_fp32_param(p), w, rtol=0, atol=0, msg=n)
-        torch.testing.assert_close(safe_get_full_optimizer_state(p, "exp_avg"), m, rtol=0, atol=0, msg=n)
-        torch.testing.assert_close(safe_get_full_optimizer_state(p, "exp_avg_sq"), v, rtol=0, atol=0, msg=n)
-    x = random_tokens(1, 2, 16, seed=4)[0]
-    loss = eng(x, labels=x)
-    eng.backward(loss)
-    eng.step()
+        full[n] = {"fp32": safe_get_full_fp32_param(p), "exp_avg": safe_get_full_optimizer_state(p, "exp_avg"),
+                   "exp_avg_sq": safe_get_full_optimizer_state(p, "exp_avg_sq")}
+    if dist.get_rank() == 0:
+        torch.save(full, out)
+
+
+# ---- the reference's reader, re-implemented --------------------------------------------------------------------
+def _ref_files(ckpt_dir):
+    optim = sorted(glob.glob(os.path.join(ckpt_dir, "*_optim_states.pt")),
+                   key=lambda f: int(re.search(r"zero_pp_rank_(\d+)", f).group(1)))
+    model = sorted(glob.glob(os.path.join(ckpt_dir, "*_model_states.pt")))
+    return optim, model
+
+
+def _ref_consolidate(ckpt_dir):
+    optim, model = _ref_files(ckpt_dir)
+    sds = [torch.load(f, map_location="cpu", weights_only=False)["optimizer_state_dict"] for f in optim]
+    ms = torch.load(model[0], map_location="cpu", weights_only=False)
+    stage = sds[0]["zero_stage"]
+    world = sds[0]["partition_count"]
+    world = max(world) if isinstance(world, list) else world
+    assert world == len(optim)
+    param_shapes = ms["param_shapes"]
+    assert isinstance(ms["shared_params"], dict) and "buffer_names" in ms
+    out = {}
+    if stage <= 2:
+        groups = [[sd["single_partition_of_fp32_groups"][i] for sd in sds] for i in range(len(param_shapes))]
+        for shapes, parts in zip(param_shapes, groups):
+            flat = torch.cat(parts, 0)
+            off = 0
+            for name, shape in shapes.items():
+                n = shape.numel()
+                out[name] = flat.narrow(0, off, n).view(shape)
+                off += n
+            align = 2 * world
+            assert math.ceil(off / align) * align == math.ceil(flat.numel() / align) * align
+    else:
+        flats = [torch.cat(sd["fp32_flat_groups"], 0) for sd in sds]
+        shapes = {k: v for d in param_shapes for k, v in d.items()}
+        off = 0
+        for name, shape in shapes.items():
+            n = shape.numel()
+            pn = math.ceil(n / world)
+            out[name] = torch.cat([flats[r].narrow(0, off, pn) for r in range(world)], 0).narrow(0, 0, n).view(shape)
+            off += pn
+        assert off * world == flats[0].numel() * world
+    return out, stage, sds, ms
+
+
+def _ref_fragments(sds, key):
+    """ds_to_universal's walk: per rank and group, every mapped fragment of `key`, concatenated per parameter."""
+    frags = {}
+    for sd in sds:
+        state = sd["base_optimizer_state"]["state"]
+        for gi, mapping in enumerate(sd["param_slice_mappings"]):
+            flat = sd["single_partition_of_fp32_groups"][gi] if key == "fp32" else state[gi][key]
+            for name, fr in mapping.items():
+                frags.setdefault(name, []).append(flat.narrow(0, fr["start"], fr["numel"]))
+    return {n: torch.cat(v) for n, v in frags.items()}
+
+
+@pytest.mark.parametrize("stage", [1, 2, 3])
+def test_reference_reader_consolidates_our_files(stage, tmp_path):
+    save, out = str(tmp_path / "ck"), str(tmp_path / "full.pt")
+    run_distributed(_train_and_save, 4, stage, save, out)
+    want = torch.load(out, weights_only=True)
+    ref_dir = os.path.join(save, "reference_format")
+    with open(os.path.join(ref_dir, "latest")) as f:
+        assert f.read().strip() == "t"
+    got, st, sds, ms = _ref_consolidate(os.path.join(ref_dir, "t"))
+    assert st == stage and len(ms["param_shapes"]) == 2  # decay / no-decay groups kept apart
+    assert set(got) == set(want)
+    for n in want:
+        torch.testing.assert_close(got[n], want[n]["fp32"], rtol=0, atol=0, msg=n)
+    if stage <= 2:
+        for key in ("fp32", "exp_avg", "exp_avg_sq"):
+            fr = _ref_fragments(sds, key)
+            for n in want:
+                torch.testing.assert_close(fr[n].view(want[n][key].shape), want[n][key], rtol=0, atol=0, msg=f"{n} {key}")
+        assert sum(sd["group_paddings"][0] for sd in sds[:-1]) == 0
+    else:
+        # moments follow the fp32 layout inside the torch-optimizer state
+        shapes = {k: v for d in ms["param_shapes"] for k, v in d.items()}
+        for key in ("exp_avg", "exp_avg_sq"):
+            flats = [torch.cat([sd["optimizer_state_dict"]["state"][g][key] for g in range(2)]) for sd in sds]
+            off = 0
+            for n, shape in shapes.items():
+                pn = math.ceil(shape.numel() / 4)
+                full = torch.cat([f.narrow(0, off, pn) for f in flats]).narrow(0, 0, shape.numel()).view(shape)
+                torch.testing.assert_close(full, want[n][key], rtol=0, atol=0, msg=f"{n} {key}")
+                off += pn
+
+
+def _resume(stage, save, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    cfg = base_config(stage=stage, lr=1e-2, mb=2)
+    model = tiny_llama()
+    decay = [p for n, p in model.named_parameters() if p.dim() >= 2]
+    no_decay = [p for n, p in model.named_parameters() if p.dim() < 2]
+    eng, _, _, _ = ds.initialize(model=model, config=cfg, model_parameters=[
+        {"params": decay, "weight_decay": 0.1}, {"params": no_decay, "weight_decay": 0.0}])
+    eng.load_checkpoint(save, tag="t")
+    losses = []
+    for x in random_tokens(2, 2, 16, seed=99):
+        loss = eng(x, labels=x)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss.detach()))
+    if dist.get_rank() == 0:
+        torch.save(losses, out)
 
 
 @pytest.mark.parametrize("stage", [2, 3])
-@pytest.mark.parametrize("world", [2, 1])
-def test_engine_loads_reference_layout(stage, world, tmp_path):
-    vals = _ref_values()
-    vp = str(tmp_path / "vals.pt")
-    torch.save(dict(vals), vp)
-    ckpt = str(tmp_path / "ck")
-    (write_reference_zero2 if stage == 2 else write_reference_zero3)(os.path.join(ckpt, "ref"), vals, 2)
-    run_distributed(_load_ref, world, stage, ckpt, "ref", vp)
+def test_engine_resumes_from_reference_format_at_another_world_size(stage, tmp_path):
+    """The files the exporter writes are read back by the engine's reference-format sources (world 4 -> 2) and give
+    the same next-step losses as resuming from the native shards."""
+    save, full = str(tmp_path / "ck"), str(tmp_path / "full.pt")
+    run_distributed(_train_and_save, 4, stage, save, full)
+    a, b = str(tmp_path / "a.pt"), str(tmp_path / "b.pt")
+    run_distributed(_resume, 2, stage, save, a)
+    run_distributed(_resume, 2, stage, os.path.join(save, "reference_format"), b)
+    assert torch.load(a, weights_only=True) == pytest.approx(torch.load(b, weights_only=True), rel=1e-6)
+
+
+def test_offline_export_to_other_world_size(tmp_path):
+    from deepspeedsyclsupport_amd.checkpoint import reference_format as rf
+    save, out = str(tmp_path / "ck"), str(tmp_path / "full.pt")
+    run_distributed(_train_and_save, 2, 2, save, out)
+    import shutil
+    shutil.rmtree(os.path.join(save, "reference_format"))
+    files = rf.export_checkpoint(save, "t", world=3)
+    assert len(files) == 3
+    got, _, _, _ = _ref_consolidate(os.path.join(save, "reference_format", "t"))
+    want = torch.load(out, weights_only=True)
+    for n in want:
+        torch.testing.assert_close(got[n], want[n]["fp32"], rtol=0, atol=0, msg=n)
