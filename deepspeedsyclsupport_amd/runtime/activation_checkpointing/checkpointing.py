@@ -10,6 +10,13 @@ MI355X notes:
 * `cpu_checkpointing`: saved inputs go to pinned host memory with a non-blocking D2H on a side HIP stream (overlaps the
   next layer's forward); the backward issues the H2D prefetch on the same stream and the compute stream waits on an
   event only when the tensor is needed. With 288 GB of HBM this is rarely required below 70B.
+* `contiguous_memory_optimization` (reference `:373-483`): the partitioned checkpoints of one iteration live in
+  pre-allocated `[number_checkpoints, partition]` buffers, one per (argument position, size, dtype, residence), filled
+  slot by slot as layers checkpoint and rewound by `reset()` at the iteration boundary — no allocator traffic and no
+  fragmentation from thousands of odd-sized slices. Host-resident buffers are pinned once.
+* `non_reentrant_checkpoint` (reference `:724`): saved-tensor hooks discard the segment's activations in forward and
+  recompute them on first use in backward; the segment INPUTS are kept by the same `_Saved` records as the reentrant
+  path, so `partition_activations`, `cpu_checkpointing` and the contiguous buffers apply to both variants.
 * RNG: the HIP generator state is captured per checkpoint and restored around recompute, so dropout masks match.
 """
 import contextlib
@@ -131,23 +138,66 @@ def _side():
     return _side_stream
 
 
-class _Saved:
-    """A checkpoint input stored partitioned across MP and/or in host memory."""
+class _ContiguousPool:
+    """Pre-allocated checkpoint storage: one `[slots, numel]` buffer per (argument position, numel, dtype, device /
+    pinned host), a cursor per buffer that `rewind()` resets every iteration. A buffer grows (doubling) when an
+    iteration checkpoints more segments than `number_checkpoints` announced."""
 
-    def __init__(self, t):
+    def __init__(self):
+        self.buffers = {}
+        self.cursor = {}
+        self.allocations = 0
+
+    def slot(self, arg_idx, numel, dtype, device, pinned):
+        key = (arg_idx, int(numel), dtype, str(device), bool(pinned))
+        i = self.cursor.get(key, 0)
+        buf = self.buffers.get(key)
+        if buf is None or i >= buf.shape[0]:
+            want = max(int(num_layers or 1), 1) if buf is None else 2 * buf.shape[0]
+            new = torch.empty((want, int(numel)), dtype=dtype, device="cpu" if pinned else device,
+                              pin_memory=bool(pinned) and get_accelerator().device_name() == "cuda")
+            if buf is not None:  # slots already handed out this iteration stay valid in the old buffer
+                self.cursor[key] = i = 0
+            self.buffers[key] = buf = new
+            self.allocations += 1
+        self.cursor[key] = i + 1
+        return buf[i]
+
+    def rewind(self):
+        self.cursor = {}
+
+
+_POOL = _ContiguousPool()
+
+
+class _Saved:
+    """A checkpoint input stored partitioned across MP and/or in host memory (optionally in the contiguous pool)."""
+
+    def __init__(self, t, arg_idx=0):
         self.requires_grad = t.requires_grad
         self.shape, self.dtype, self.device = t.shape, t.dtype, t.device
         data = t.detach()
         self.partitioned = PARTITION_ACTIVATIONS and mp_size > 1 and data.numel() % mp_size == 0
+        self.on_host = CPU_CHECKPOINT and data.is_cuda
+        pooled = CONTIGUOUS_CHECKPOINTING and self.partitioned
+        self.pooled = pooled
         if self.partitioned:
             flat = data.reshape(-1)
             n = flat.numel() // mp_size
-            data = flat[mp_rank * n:(mp_rank + 1) * n].clone()
-        self.on_host = CPU_CHECKPOINT and data.is_cuda
+            part = flat[mp_rank * n:(mp_rank + 1) * n]
+            if pooled and not self.on_host:
+                dst = _POOL.slot(arg_idx, n, data.dtype, data.device, False)
+                dst.copy_(part)
+                data = dst
+            else:
+                data = part.clone() if not self.on_host else part
         self.event = None
         if self.on_host:
             s = _side()
-            host = torch.empty(data.shape, dtype=data.dtype, pin_memory=True)
+            if pooled:
+                host = _POOL.slot(arg_idx, data.numel(), data.dtype, data.device, True).view(data.shape)
+            else:
+                host = torch.empty(data.shape, dtype=data.dtype, pin_memory=True)
             s.wait_stream(get_accelerator().current_stream())
             with get_accelerator().stream(s):
                 host.copy_(data, non_blocking=True)
@@ -185,7 +235,7 @@ class CheckpointFunction(torch.autograd.Function):
         ctx.fwd_cpu_state = torch.get_rng_state()
         ctx.fwd_dev_state = _device_rng_state()
         ctx.fwd_tracker_states = get_cuda_rng_tracker().get_states()
-        ctx.saved = [(_Saved(a) if torch.is_tensor(a) else a) for a in args]
+        ctx.saved = [(_Saved(a, i) if torch.is_tensor(a) else a) for i, a in enumerate(args)]
         with torch.no_grad():
             outputs = run_function(*args)
         if SYNCHRONIZE:
@@ -228,9 +278,41 @@ def checkpoint(function, *args):
 
 
 def non_reentrant_checkpoint(function, *args):
-    """Non-reentrant variant built on torch's saved-tensor machinery (reference `:724`)."""
+    """Non-reentrant checkpoint (reference `:724`): the forward runs WITH a graph whose saved activations are
+    discarded by saved-tensor hooks; the first backward node that needs one triggers a recompute of the segment
+    (torch's hook machinery, which also stops the recompute as soon as every needed tensor is back). The segment's
+    inputs are held the same way as in the reentrant path — partitioned across the tensor-parallel group, in pinned
+    host memory, in the contiguous pool — and re-assembled for the recompute; RNG states are replayed so dropout
+    repeats."""
     import torch.utils.checkpoint as cp
-    return cp.checkpoint(function, *args, use_reentrant=False)
+    holder = {"args": args, "saved": None}
+    fwd_cpu_state = torch.get_rng_state()
+    fwd_dev_state = _device_rng_state()
+    fwd_tracker_states = get_cuda_rng_tracker().get_states()
+
+    def run():
+        if holder["args"] is not None:  # the forward pass itself
+            return function(*holder["args"])
+        inputs = [s.restore() if isinstance(s, _Saved) else s for s in holder["saved"]]
+        bwd_cpu_state = torch.get_rng_state()
+        bwd_dev_state = _device_rng_state()
+        bwd_tracker_states = get_cuda_rng_tracker().get_states()
+        torch.set_rng_state(fwd_cpu_state)
+        _set_device_rng_state(fwd_dev_state)
+        get_cuda_rng_tracker().set_states(fwd_tracker_states)
+        try:
+            return function(*inputs)
+        finally:  # also on the early stop torch raises once the last needed activation is recomputed
+            torch.set_rng_state(bwd_cpu_state)
+            _set_device_rng_state(bwd_dev_state)
+            get_cuda_rng_tracker().set_states(bwd_tracker_states)
+
+    out = cp.checkpoint(run, use_reentrant=False, preserve_rng_state=False)
+    holder["saved"] = [(_Saved(a, i) if torch.is_tensor(a) else a) for i, a in enumerate(args)]
+    holder["args"] = None
+    if SYNCHRONIZE:
+        get_accelerator().synchronize()
+    return out
 
 
 def partition_activations_in_checkpoint(partition_activation):
@@ -244,8 +326,9 @@ def set_num_layers(nlayers):
 
 
 def reset():
-    """Per-iteration reset (no contiguous buffers are kept in this implementation)."""
-    return None
+    """Iteration boundary (reference `:1004`): rewind the contiguous checkpoint buffers so the next forward refills
+    them from slot 0. Call it once per training step when `contiguous_memory_optimization` is on (the engine does)."""
+    _POOL.rewind()
 
 
 def configure(mpu_, deepspeed_config=None, partition_activations=None, contiguous_checkpointing=None,
@@ -284,6 +367,7 @@ def configure(mpu_, deepspeed_config=None, partition_activations=None, contiguou
         mp_rank, mp_size, mp_group = 0, 1, None
     if CONTIGUOUS_CHECKPOINTING:
         assert PARTITION_ACTIVATIONS, "Contiguous Checkpointing is only available with partitioned activations."
+        assert num_layers is not None, "Must specify the number of layers with contiguous memory checkpointing"
 
 
 def is_configured():

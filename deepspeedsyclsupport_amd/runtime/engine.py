@@ -594,6 +594,9 @@ class DeepSpeedEngine(nn.Module):
         self.timers(STEP_MICRO_TIMER).start()
         if self.is_gradient_accumulation_boundary():
             self.gas_boundary_ctr += 1
+            from .activation_checkpointing import checkpointing as _ckpt
+            if _ckpt.CONTIGUOUS_CHECKPOINTING:
+                _ckpt.reset()  # every checkpoint of this step has been consumed: refill the buffers from slot 0
             if self.progressive_layer_drop is not None:
                 self.progressive_layer_drop.update_state(self.global_steps)
             if self.optimizer is not None:
