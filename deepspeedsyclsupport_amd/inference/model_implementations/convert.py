@@ -353,6 +353,107 @@ def _phi(model):
     return spec, top, layers
 
 
+def _megatron_parts(model):
+    """(embedding, transformer stack) of a Megatron-LM GPT model, or None. Duck-typed on the attribute names the
+    reference's policy keys on (`module_inject/containers/megatron_gpt.py:36-140`): Megatron is not a dependency."""
+    lm = getattr(model, "language_model", None)
+    if lm is None:
+        return None
+    emb = getattr(lm, "embedding", None)
+    tr = getattr(lm, "encoder", None) or getattr(lm, "transformer", None)
+    if emb is None or tr is None or not hasattr(emb, "word_embeddings") or not len(getattr(tr, "layers", [])):
+        return None
+    first = tr.layers[0]
+    attn = getattr(first, "self_attention", None) or getattr(first, "attention", None)
+    if attn is None or not hasattr(attn, "query_key_value") or not hasattr(first, "input_layernorm"):
+        return None
+    return emb, tr
+
+
+def _megatron_gpt(model):
+    """Megatron-LM GPT and GPT-MoE (reference containers `module_inject/containers/megatron_gpt.py`,
+    `megatron_gpt_moe.py`; inference modules `ds_megatron_gpt.py`, `moe_inference.py`).
+
+    * layers: `input_layernorm`, `self_attention.query_key_value` (`attention.` in the oldest Megatron sources) +
+      `.dense`, `post_attention_layernorm`, `mlp.dense_h_to_4h` / `mlp.dense_4h_to_h`; learned positions, LayerNorm,
+      tanh-GELU (Megatron's fused bias-gelu), LM head tied to the word embeddings.
+    * fused QKV rows: Megatron v2 orders them [head, (q, k, v), head_dim]; older checkpoints [(q, k, v), head,
+      head_dim] (`model.megatron_v2 = False`, reference `MegatronContainer.transpose_qkv_alignment`).
+    * MoE layers (`mlp.deepspeed_moe`): top-1 gate `gate.wg`, experts `experts.deepspeed_experts[i]` as biased dense
+      MLPs, output scaled by the gate probability; residual MoE (`mlp.moe.deepspeed_moe` + `mlp.mlp` +
+      `mlp.coefficient`, PR-MoE) mixes the experts with a dense MLP. Every layer of the model must be of one kind
+      (the inference stack is homogeneous); a dense / MoE mix raises.
+    """
+    emb, tr = _megatron_parts(model)
+    first = tr.layers[0]
+    old = not hasattr(first, "self_attention")
+    attn0 = first.attention if old else first.self_attention
+    V, H = emb.word_embeddings.weight.shape
+    nh = getattr(attn0, "num_attention_heads", None) or attn0.num_attention_heads_per_partition
+    hd = H // nh
+    v2 = bool(getattr(model, "megatron_v2", not old))
+
+    def experts_of(mlp):
+        if hasattr(mlp, "deepspeed_moe"):
+            return mlp.deepspeed_moe, None
+        if hasattr(mlp, "moe") and hasattr(mlp.moe, "deepspeed_moe"):
+            return mlp.moe.deepspeed_moe, mlp
+        return None, None
+
+    kinds = {("res" if experts_of(L.mlp)[1] is not None else "moe") if experts_of(L.mlp)[0] is not None else "dense"
+             for L in tr.layers}
+    if len(kinds) != 1:
+        raise NotImplementedError(f"Megatron model mixes {sorted(kinds)} MLP layers: kernel injection needs every "
+                                  f"layer to be of one kind")
+    kind = kinds.pop()
+    moe0, _ = experts_of(first.mlp)
+    if moe0 is not None:
+        ex0 = moe0.experts.deepspeed_experts
+        E, I = len(ex0), ex0[0].dense_h_to_4h.weight.shape[0]
+        k = int(getattr(moe0.gate, "k", 1))
+    else:
+        E, I, k = 0, first.mlp.dense_h_to_4h.weight.shape[0], 1
+    spec = DSModelSpec(arch="megatron_gpt" + ("_moe" if E else ""), vocab_size=V, hidden_size=H,
+                       num_layers=len(tr.layers), num_heads=nh, num_kv_heads=nh, intermediate_size=I, norm="ln",
+                       norm_eps=float(getattr(first.input_layernorm, "eps", 1e-5)), pos="learned", act="gelu_tanh",
+                       gated_mlp=False, qkv_bias=True, o_bias=True, mlp_bias=True,
+                       max_positions=emb.position_embeddings.weight.shape[0], tie_embeddings=True, num_experts=E,
+                       moe_top_k=k, moe_renormalize=False, moe_residual=kind == "res")
+    layers = []
+    for L in tr.layers:
+        at = L.attention if old else L.self_attention
+        w, b = at.query_key_value.weight, at.query_key_value.bias
+        if v2:
+            q, kk, v = _split_interleaved(w, nh, hd)
+            qb, kb, vb = _split_interleaved(b, nh, hd)
+        else:
+            q, kk, v = w.split(H, 0)
+            qb, kb, vb = b.split(H, 0)
+        lw = dict(ln1_w=L.input_layernorm.weight, ln1_b=L.input_layernorm.bias,
+                  ln2_w=L.post_attention_layernorm.weight, ln2_b=L.post_attention_layernorm.bias,
+                  q_w=q, k_w=kk, v_w=v, q_b=qb, k_b=kb, v_b=vb, o_w=at.dense.weight, o_b=at.dense.bias)
+        moe, outer = experts_of(L.mlp)
+        if moe is None:
+            lw.update(fc1_w=L.mlp.dense_h_to_4h.weight, fc1_b=L.mlp.dense_h_to_4h.bias,
+                      fc2_w=L.mlp.dense_4h_to_h.weight, fc2_b=L.mlp.dense_4h_to_h.bias)
+        else:
+            ex = moe.experts.deepspeed_experts
+            lw.update(router_w=moe.gate.wg.weight,
+                      experts_fc1=torch.stack([e.dense_h_to_4h.weight for e in ex]),
+                      experts_fc1_b=torch.stack([e.dense_h_to_4h.bias for e in ex]),
+                      experts_down=torch.stack([e.dense_4h_to_h.weight for e in ex]),
+                      experts_down_b=torch.stack([e.dense_4h_to_h.bias for e in ex]))
+            if outer is not None:
+                lw.update(res_fc1_w=outer.mlp.dense_h_to_4h.weight, res_fc1_b=outer.mlp.dense_h_to_4h.bias,
+                          res_fc2_w=outer.mlp.dense_4h_to_h.weight, res_fc2_b=outer.mlp.dense_4h_to_h.bias,
+                          coef_w=outer.coefficient.weight, coef_b=getattr(outer.coefficient, "bias", None))
+        layers.append(lw)
+    fl = tr.final_layernorm
+    top = dict(embed=emb.word_embeddings.weight, pos_embed=emb.position_embeddings.weight, norm_w=fl.weight,
+               norm_b=fl.bias, lm_head=emb.word_embeddings.weight)
+    return spec, top, layers
+
+
 CONVERTERS = {
     "llama": _llama_like, "mistral": _llama_like, "qwen2": _llama_like, "internlm": _llama_like,
     "gpt2": _gpt2, "bloom": _bloom, "opt": _opt, "gpt_neox": _gpt_neox, "gptj": _gptj,
@@ -364,6 +465,8 @@ def supported(model):
     from ...models.llama import LlamaForCausalLM as NativeLlama
     if isinstance(model, NativeLlama):
         return True
+    if _megatron_parts(model) is not None:
+        return True
     mt = getattr(getattr(model, "config", None), "model_type", None)
     return mt in CONVERTERS
 
@@ -372,6 +475,8 @@ def extract(model):
     from ...models.llama import LlamaForCausalLM as NativeLlama
     if isinstance(model, NativeLlama):
         return _native_llama(model)
+    if _megatron_parts(model) is not None:
+        return _megatron_gpt(model)
     mt = model.config.model_type
     if mt not in CONVERTERS:
         raise NotImplementedError(f"no kernel-injection policy for model_type={mt!r}")
@@ -420,6 +525,19 @@ def shard_layer(spec, lw, r, tp):
         out["fc1_w"] = torch.cat([gu[:, r * n:(r + 1) * n], gu[:, I + r * n:I + (r + 1) * n]], 1)
         out["fc2_w"] = lw["experts_down"][:, :, r * n:(r + 1) * n]
         out["router_w"] = lw["router_w"]
+    elif "experts_fc1" in lw:  # Megatron-style experts: plain biased MLPs [E, I, H] / [E, H, I]
+        n = lw["experts_fc1"].shape[1] // tp
+        out["fc1_w"] = lw["experts_fc1"][:, r * n:(r + 1) * n]
+        out["fc1_b"] = lw["experts_fc1_b"][:, r * n:(r + 1) * n]
+        out["fc2_w"] = lw["experts_down"][:, :, r * n:(r + 1) * n]
+        out["fc2_b"] = lw["experts_down_b"] / tp  # every TP rank adds its share; the all-reduce restores the bias
+        out["router_w"] = lw["router_w"]
+        if "res_fc1_w" in lw:
+            out["res_fc1_w"], out["res_fc1_b"] = _rows(lw["res_fc1_w"], r, tp), _rows(lw["res_fc1_b"], r, tp)
+            out["res_fc2_w"], out["res_fc2_b"] = _cols(lw["res_fc2_w"], r, tp), lw["res_fc2_b"]
+            out["coef_w"] = lw["coef_w"]
+            if lw.get("coef_b") is not None:
+                out["coef_b"] = lw["coef_b"]
     elif "gate_w" in lw:
         out["fc1_w"] = torch.cat([_rows(lw["gate_w"], r, tp), _rows(lw["up_w"], r, tp)], 0)
         if lw.get("gate_b") is not None:
@@ -430,7 +548,7 @@ def shard_layer(spec, lw, r, tp):
             out["fc1_b"] = _rows(lw["fc1_b"], r, tp)
     if "experts_down" not in lw:
         out["fc2_w"] = _cols(lw["fc2_w"], r, tp)
-    if lw.get("fc2_b") is not None:
+    if lw.get("fc2_b") is not None and "experts_down" not in lw:
         out["fc2_b"] = lw["fc2_b"]
     for n in ("ln1_w", "ln1_b", "ln2_w", "ln2_b"):
         if lw.get(n) is not None:

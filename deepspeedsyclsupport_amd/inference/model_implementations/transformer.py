@@ -59,6 +59,7 @@ class DSModelSpec:
     num_experts: int = 0             # > 0: MoE MLP (Mixtral-style top-k router over gated experts)
     moe_top_k: int = 2
     moe_renormalize: bool = True     # renormalise the top-k routing weights to sum to 1
+    moe_residual: bool = False       # PR-MoE: softmax(coefficient(x)) mixes the routed experts with a dense MLP
 
     def __post_init__(self):
         if not self.head_dim:
@@ -222,8 +223,19 @@ class DSInferenceLayer(nn.Module):
             self.router_w = None
             self.fc1_w = nn.Parameter(torch.empty(G * I, H, **kw), requires_grad=False)
             self.fc2_w = nn.Parameter(torch.empty(H, I, **kw), requires_grad=False)
-        self.fc1_b = nn.Parameter(torch.zeros(G * I, **kw), requires_grad=False) if spec.mlp_bias and not E else None
-        self.fc2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.mlp_bias and not E else None
+        if E:  # per-expert biases (Megatron-style experts); fc2's is pre-divided by the TP degree (summed back)
+            self.fc1_b = nn.Parameter(torch.zeros(E, G * I, **kw), requires_grad=False) if spec.mlp_bias else None
+            self.fc2_b = nn.Parameter(torch.zeros(E, H, **kw), requires_grad=False) if spec.mlp_bias else None
+        else:
+            self.fc1_b = nn.Parameter(torch.zeros(G * I, **kw), requires_grad=False) if spec.mlp_bias else None
+            self.fc2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False) if spec.mlp_bias else None
+        if E and spec.moe_residual:  # dense MLP beside the experts + the 2-way mixing coefficient
+            self.res_fc1_w = nn.Parameter(torch.empty(G * I, H, **kw), requires_grad=False)
+            self.res_fc1_b = nn.Parameter(torch.zeros(G * I, **kw), requires_grad=False)
+            self.res_fc2_w = nn.Parameter(torch.empty(H, I, **kw), requires_grad=False)
+            self.res_fc2_b = nn.Parameter(torch.zeros(H, **kw), requires_grad=False)
+            self.coef_w = nn.Parameter(torch.empty(2, H, **kw), requires_grad=False)
+            self.coef_b = nn.Parameter(torch.zeros(2, **kw), requires_grad=False)
         self.quant = {}
         # split (aliased) projections: name -> list of weights / biases applied side by side (hybrid engine shares
         # the training module's separate q/k/v and gate/up tensors instead of fusing copies)
@@ -356,7 +368,14 @@ class DSInferenceLayer(nn.Module):
         MFMA GEMM pair -> weighted gather, all on device without a host sync (`ops/moe_ops.py`). Experts are
         TP-sharded along the intermediate dim, so one all-reduce finishes the block exactly like a dense MLP."""
         out = moe_ops.moe_block(x, self.router_w, self.fc1_w, self.fc2_w, self.spec.moe_top_k, self._act,
-                                self.spec.moe_renormalize)
+                                self.spec.moe_renormalize, fc1_b=self.fc1_b, fc2_b=self.fc2_b)
+        if self.spec.moe_residual:
+            # PR-MoE (reference `ops/transformer/inference/moe_inference.py:300-330`, `moe_res_matmul`): the dense
+            # branch is TP-sharded like the experts, so both are summed by the one all-reduce below
+            dense = F.linear(self._act(F.linear(x, self.res_fc1_w, self.res_fc1_b)), self.res_fc2_w)
+            coef = torch.softmax(F.linear(x, self.coef_w, self.coef_b).float(), -1).to(x.dtype)
+            out = self._allreduce(out * coef[..., 0:1] + dense * coef[..., 1:2])
+            return out + self.res_fc2_b * coef[..., 1:2]
         return self._allreduce(out)
 
     def _mlp(self, x):

@@ -30,8 +30,9 @@ def topk_gating_reference(logits, k, renormalize=False):
     return w, e, torch.bincount(e.reshape(-1), minlength=logits.shape[-1])
 
 
-def moe_block_reference(x, router_w, fc1_w, fc2_w, k, act, renormalize=False, routing=None):
-    """out[t] = sum_j w[t, j] * fc2_e(act(fc1_e(x[t]))) with e = experts[t, j]; fp32 accumulation.
+def moe_block_reference(x, router_w, fc1_w, fc2_w, k, act, renormalize=False, routing=None, fc1_b=None, fc2_b=None):
+    """out[t] = sum_j w[t, j] * fc2_e(act(fc1_e(x[t]))) with e = experts[t, j]; fp32 accumulation. Optional
+    per-expert biases fc1_b [E, N1] / fc2_b [E, H] (Megatron-style experts).
     `routing=(w, e)` replaces the router (tests feed the device gating's choice to isolate the expert math)."""
     t = x.reshape(-1, x.shape[-1])
     if routing is None:
@@ -50,8 +51,8 @@ def moe_block_reference(x, router_w, fc1_w, fc2_w, k, act, renormalize=False, ro
             continue
         rows, ww = tok[s:s + c], wts[s:s + c]
         s += c
-        h = act(F.linear(t.index_select(0, rows), fc1_w[ex]))
-        y = F.linear(h, fc2_w[ex])
+        h = act(F.linear(t.index_select(0, rows), fc1_w[ex], None if fc1_b is None else fc1_b[ex]))
+        y = F.linear(h, fc2_w[ex], None if fc2_b is None else fc2_b[ex])
         out.index_add_(0, rows, y.float() * ww[:, None])
     return out.to(x.dtype).view(x.shape)
 
@@ -97,19 +98,29 @@ def native_moe_ok(x, router_w, fc1_w, fc2_w, k):
             and grouped_gemm_ok(fc1_w.shape[1], fc1_w.shape[2]) and grouped_gemm_ok(fc2_w.shape[1], fc2_w.shape[2]))
 
 
-def moe_block(x, router_w, fc1_w, fc2_w, k, act, renormalize=False):
+def moe_block(x, router_w, fc1_w, fc2_w, k, act, renormalize=False, fc1_b=None, fc2_b=None):
     """Routed expert MLP of a ragged token batch. `act` maps fc1 output [R, G*I] -> [R, I] (gated or plain).
+    fc1_b [E, G*I] / fc2_b [E, H]: optional per-expert biases.
 
-    Device path: gating -> scatter -> grouped GEMM -> act -> grouped GEMM -> weighted gather (bf16 out).
+    Device path: gating -> scatter -> grouped GEMM -> act -> grouped GEMM -> weighted gather (bf16 out); expert
+    biases are added to the expert-contiguous rows through a sync-free row -> expert map.
     """
     if not native_moe_ok(x, router_w, fc1_w, fc2_w, k):
-        return moe_block_reference(x, router_w, fc1_w, fc2_w, k, act, renormalize)
+        return moe_block_reference(x, router_w, fc1_w, fc2_w, k, act, renormalize, fc1_b=fc1_b, fc2_b=fc2_b)
     shp = x.shape
     t = x.reshape(-1, shp[-1]).contiguous()
     scores, experts, slots, counts = topk_gating(F.linear(t, router_w), k, renormalize)
     xs, rows, _ = moe_scatter(t, experts, slots, counts)
-    h = act(grouped_gemm(xs, fc1_w, counts))
-    y = grouped_gemm(h, fc2_w, counts)
+    h = grouped_gemm(xs, fc1_w, counts)
+    row_expert = None
+    if fc1_b is not None or fc2_b is not None:
+        row_expert = torch.repeat_interleave(torch.arange(counts.numel(), device=counts.device), counts.long(),
+                                             output_size=xs.shape[0])
+    if fc1_b is not None:
+        h = h + fc1_b.index_select(0, row_expert)
+    y = grouped_gemm(act(h), fc2_w, counts)
+    if fc2_b is not None:
+        y = y + fc2_b.index_select(0, row_expert)
     return moe_gather(y, scores, rows).view(shp)
 
 

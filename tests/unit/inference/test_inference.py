@@ -147,6 +147,36 @@ def test_native_llama_injection():
     assert (eng(ids).logits - ref).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("kind", ["llama", "gpt2", "bloom"])
+def test_revert_transformer_layer_round_trip(kind):
+    """replace -> edit the injected weights -> revert: the original module comes back carrying the edit (reference
+    `module_inject/replace_module.py` revert_transformer_layer)."""
+    from deepspeedsyclsupport_amd.inference.config import DeepSpeedInferenceConfig
+    from deepspeedsyclsupport_amd.module_inject import replace_transformer_layer, revert_transformer_layer
+    m = tiny(kind).eval()
+    ids = _ids()
+    cfg = DeepSpeedInferenceConfig(dtype="fp32")
+    inj = replace_transformer_layer(None, m, config=cfg)
+    with torch.no_grad():
+        ref = m(ids).logits.clone()
+        back = revert_transformer_layer(None, inj, cfg)
+        assert back is m
+        assert (m(ids).logits - ref).abs().max().item() < 1e-5  # an unedited round trip changes nothing
+        for layer in inj.layers:
+            layer.o_w.mul_(0.5)
+            layer.fc2_w.mul_(2.0)
+        revert_transformer_layer(None, inj, cfg)
+        from deepspeedsyclsupport_amd.inference.model_implementations import convert
+        _, _, lws = convert.extract(m)
+        for lw, layer in zip(lws, inj.layers):
+            torch.testing.assert_close(lw["o_w"].contiguous(), layer.o_w.data, rtol=0, atol=0)
+            if "fc2_w" in lw:
+                torch.testing.assert_close(lw["fc2_w"].contiguous(), layer.fc2_w.data, rtol=0, atol=0)
+        assert (m(ids).logits - ref).abs().max().item() > 1e-4  # and the original model now computes with them
+    with pytest.raises(ValueError):
+        revert_transformer_layer(None, torch.nn.Linear(2, 2), cfg)
+
+
 def test_config_aliases():
     from deepspeedsyclsupport_amd.inference.config import DeepSpeedInferenceConfig
     c = DeepSpeedInferenceConfig(kernel_inject=True, dtype="bf16", mp_size=2, max_tokens=77)
