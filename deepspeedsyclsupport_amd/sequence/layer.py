@@ -67,28 +67,47 @@ class DistributedAttention(torch.nn.Module):
 
 
 # ---------------------------------------------------------------------------------------------- fused [B,H,S,D] path
+# Copy budget. all_to_all_single fixes both buffer layouts ([P, ...]: one contiguous chunk per peer), and the flash
+# kernels need a uniform token stride, so each direction costs exactly one packing pass into the send buffer and one
+# unpacking pass out of the receive buffer. Everything else is views: the packed buffer is filled by strided copies
+# straight from whatever layout the producer left (no cat / contiguous staging), and the unpacked [B, heads, S, D]
+# buffer is handed to attention as per-tensor views (the kernels take batch / head / token strides).
+def _pack(dst, src):
+    """One strided copy (a single HBM pass) of a view into (a view of) a communication buffer."""
+    dst.copy_(src)
+
+
 def _heads_to_seq(q, k, v, group):
-    """[B,Hq,s,D],[B,Hk,s,D],[B,Hk,s,D] (local tokens) -> [B,Hq/P,S,D], ... (local heads, all tokens). One a2a."""
+    """[B,Hq,s,D],[B,Hk,s,D],[B,Hk,s,D] (local tokens) -> views [B,Hq/P,S,D], ... (local heads, all tokens) of one
+    receive buffer. One a2a, one pass in, one pass out."""
     P = dist.get_world_size(group)
     B, Hq, s, D = q.shape
     Hk = k.shape[1]
     hq, hk = Hq // P, Hk // P
+    h3 = hq + 2 * hk
     # send[p] = [q heads of rank p | k heads of rank p | v heads of rank p], each [B, h, s, D]
-    send = torch.cat([q.view(B, P, hq, s, D), k.view(B, P, hk, s, D), v.view(B, P, hk, s, D)], dim=2)
-    send = send.transpose(0, 1).contiguous()  # [P, B, hq+2hk, s, D]
+    send = torch.empty((P, B, h3, s, D), dtype=q.dtype, device=q.device)
+    _pack(send[:, :, :hq], q.unflatten(1, (P, hq)).transpose(0, 1))
+    _pack(send[:, :, hq:hq + hk], k.unflatten(1, (P, hk)).transpose(0, 1))
+    _pack(send[:, :, hq + hk:], v.unflatten(1, (P, hk)).transpose(0, 1))
     recv = _a2a(send, group)  # recv[p] = rank p's tokens of my heads
-    recv = recv.permute(1, 2, 0, 3, 4).reshape(B, hq + 2 * hk, P * s, D)  # token order = rank order
-    return recv[:, :hq], recv[:, hq:hq + hk], recv[:, hq + hk:]
+    full = torch.empty((B, h3, P, s, D), dtype=q.dtype, device=q.device)  # token order = rank order
+    _pack(full, recv.permute(1, 2, 0, 3, 4))
+    full = full.view(B, h3, P * s, D)
+    return full[:, :hq], full[:, hq:hq + hk], full[:, hq + hk:]
 
 
 def _seq_to_heads(o, group):
-    """[B, h, S, D] (local heads, all tokens) -> [B, h*P, S/P, D] (all heads, local tokens)."""
+    """[B, h, S, D] (local heads, all tokens; any strides) -> [B, h*P, S/P, D] (all heads, local tokens)."""
     P = dist.get_world_size(group)
     B, h, S, D = o.shape
     s = S // P
-    send = o.view(B, h, P, s, D).permute(2, 0, 1, 3, 4).contiguous()  # [P, B, h, s, D]
+    send = torch.empty((P, B, h, s, D), dtype=o.dtype, device=o.device)
+    _pack(send, o.unflatten(2, (P, s)).permute(2, 0, 1, 3, 4))
     recv = _a2a(send, group)  # recv[p] = rank p's heads for my tokens
-    return recv.permute(1, 0, 2, 3, 4).reshape(B, P * h, s, D)
+    out = torch.empty((B, P, h, s, D), dtype=o.dtype, device=o.device)
+    _pack(out, recv.transpose(0, 1))
+    return out.view(B, P * h, s, D)
 
 
 class _FusedQKVToSeq(torch.autograd.Function):
@@ -96,9 +115,7 @@ class _FusedQKVToSeq(torch.autograd.Function):
     @staticmethod
     def forward(ctx, group, q, k, v):
         ctx.group = group
-        ctx.hq, ctx.hk = q.shape[1], k.shape[1]
-        qo, ko, vo = _heads_to_seq(q, k, v, group)
-        return qo.contiguous(), ko.contiguous(), vo.contiguous()
+        return _heads_to_seq(q, k, v, group)
 
     @staticmethod
     def backward(ctx, dq, dk, dv):
@@ -107,13 +124,18 @@ class _FusedQKVToSeq(torch.autograd.Function):
         B, hq, S, D = dq.shape
         hk = dk.shape[1]
         s = S // P
-        g = torch.cat([dq, dk, dv], dim=1).view(B, hq + 2 * hk, P, s, D).permute(2, 0, 1, 3, 4).contiguous()
+        h3 = hq + 2 * hk
+        g = torch.empty((P, B, h3, s, D), dtype=dq.dtype, device=dq.device)
+        _pack(g[:, :, :hq], dq.unflatten(2, (P, s)).permute(2, 0, 1, 3, 4))
+        _pack(g[:, :, hq:hq + hk], dk.unflatten(2, (P, s)).permute(2, 0, 1, 3, 4))
+        _pack(g[:, :, hq + hk:], dv.unflatten(2, (P, s)).permute(2, 0, 1, 3, 4))
         r = _a2a(g, ctx.group)  # r[p] = grads for rank p's heads, my tokens: [P, B, hq+2hk, s, D]
-        r = r.transpose(0, 1)  # [B, P, hq+2hk, s, D]
-        gq = r[:, :, :hq].reshape(B, P * hq, s, D)
-        gk = r[:, :, hq:hq + hk].reshape(B, P * hk, s, D)
-        gv = r[:, :, hq + hk:].reshape(B, P * hk, s, D)
-        return None, gq.contiguous(), gk.contiguous(), gv.contiguous()
+        outs = []
+        for lo, h in ((0, hq), (hq, hk), (hq + hk, hk)):  # unpack each tensor straight into its own [B, P*h, s, D]
+            t = torch.empty((B, P, h, s, D), dtype=dq.dtype, device=dq.device)
+            _pack(t, r[:, :, lo:lo + h].transpose(0, 1))
+            outs.append(t.view(B, P * h, s, D))
+        return (None, *outs)
 
 
 class _SeqToHeads(torch.autograd.Function):
@@ -128,9 +150,12 @@ class _SeqToHeads(torch.autograd.Function):
         P = dist.get_world_size(ctx.group)
         B, H, s, D = g.shape
         h = H // P
-        send = g.reshape(B, P, h, s, D).transpose(0, 1).contiguous()  # [P, B, h, s, D] -> rank p gets its heads
+        send = torch.empty((P, B, h, s, D), dtype=g.dtype, device=g.device)  # rank p gets its heads
+        _pack(send, g.unflatten(1, (P, h)).transpose(0, 1))
         recv = _a2a(send, ctx.group)  # recv[p] = my heads, rank p's tokens
-        return None, recv.permute(1, 2, 0, 3, 4).reshape(B, h, P * s, D).contiguous()
+        out = torch.empty((B, h, P, s, D), dtype=g.dtype, device=g.device)
+        _pack(out, recv.permute(1, 2, 0, 3, 4))
+        return None, out.view(B, h, P * s, D)
 
 
 class UlyssesAttention(torch.nn.Module):
@@ -150,7 +175,7 @@ class UlyssesAttention(torch.nn.Module):
             f"Ulysses needs heads divisible by sp={P} (q heads {q.shape[1]}, kv heads {k.shape[1]})"
         qs, ks, vs = _FusedQKVToSeq.apply(self.spg, q, k, v)
         o = self.attn_fn(qs, ks, vs, causal=self.causal)
-        return _SeqToHeads.apply(self.spg, o.contiguous())
+        return _SeqToHeads.apply(self.spg, o)
 
 
 def shard_sequence(input_ids, labels=None, group=None, ignore_index=-100):
