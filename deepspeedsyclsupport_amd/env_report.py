@@ -22,8 +22,8 @@ def op_report(verbose=True):
     print(f"{'op name':<24}{'extension':<14}{'built':<16}{'compatible':<16}")
     print("-" * 80)
     for name, b in sorted(op_builder.ALL_OPS.items()):
-        ext = b.EXT
-        built = OKAY if op_builder.is_built(ext) else f"{YELLOW}[NO]{END}"
+        ext = b.EXT or "(python)"  # builders without native code have nothing to build
+        built = OKAY if b.EXT is None or op_builder.is_built(b.EXT) else f"{YELLOW}[NO]{END}"
         compat = OKAY if b().is_compatible() else FAIL
         print(f"{name:<24}{ext:<14}{built:<25}{compat}")
     print("-" * 80)

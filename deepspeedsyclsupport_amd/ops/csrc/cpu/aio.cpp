@@ -126,21 +126,22 @@ class AioHandle {
     return run(buffer, filename, true, async);
   }
 
-  // wait for all outstanding async ops; returns number completed
+  // wait for all outstanding async ops; returns the number of operations (pread / pwrite calls, not their pieces)
+  // completed, as the reference's handle does
   int64_t wait() {
     std::vector<std::future<int64_t>> pend;
     std::vector<int> fds;
+    int64_t n = 0;
     {
       std::lock_guard<std::mutex> lk(mu_);
       pend.swap(pending_);
       fds.swap(open_fds_);
+      n = pending_ops_;
+      pending_ops_ = 0;
     }
-    int64_t n = 0;
     bool failed = false;
-    for (auto& f : pend) {
+    for (auto& f : pend)
       if (f.get() < 0) failed = true;
-      ++n;
-    }
     for (int fd : fds) ::close(fd);
     if (failed) throw std::runtime_error("aio: an asynchronous I/O operation failed");
     return n;
@@ -199,6 +200,7 @@ class AioHandle {
     if (async) {
       std::lock_guard<std::mutex> lk(mu_);
       for (auto& f : futs) pending_.push_back(std::move(f));
+      ++pending_ops_;
       open_fds_.push_back(fd);
       return 0;
     }
@@ -221,6 +223,7 @@ class AioHandle {
   ThreadPool pool_;
   std::mutex mu_;
   std::vector<std::future<int64_t>> pending_;
+  int64_t pending_ops_ = 0;
   std::vector<int> open_fds_;
 };
 
@@ -251,7 +254,7 @@ void register_aio(pybind11::module& m) {
   pybind11::class_<AioHandle>(m, "aio_handle")
       .def(pybind11::init<int64_t, int64_t, bool, bool, int64_t>(), pybind11::arg("block_size") = 1048576,
            pybind11::arg("queue_depth") = 128, pybind11::arg("single_submit") = false,
-           pybind11::arg("overlap_events") = false, pybind11::arg("thread_count") = 1)
+           pybind11::arg("overlap_events") = false, pybind11::arg("num_threads") = 1)
       .def("get_block_size", &AioHandle::get_block_size)
       .def("get_queue_depth", &AioHandle::get_queue_depth)
       .def("get_single_submit", &AioHandle::get_single_submit)

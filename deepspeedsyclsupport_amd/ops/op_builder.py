@@ -245,6 +245,7 @@ _BUILDERS = {
     "CPULionBuilder": ("cpu_lion", "ds_cpu_ops"),
     "AsyncIOBuilder": ("async_io", "ds_cpu_ops"),
     "ShareMemCommBuilder": ("deepspeed_shm_comm", "ds_cpu_ops"),
+    "CCLCommBuilder": ("deepspeed_ccl_comm", "ds_cpu_ops"),  # reference name of the CPU shared-memory collectives op
     "RandomLTDBuilder": ("random_ltd", "ds_hip_ops"),
     "SpatialInferenceBuilder": ("spatial_inference", "ds_hip_ops"),
     "SparseAttnBuilder": ("sparse_attn", "ds_hip_ops"),

@@ -69,24 +69,30 @@ class DynamicLossScaler(LossScalerBase):
         self.dynamic = True
         self.dtype = dtype
 
+    def _shrink(self):
+        if self.cur_scale == self.min_scale and self.raise_error_at_min_scale:
+            raise Exception("Current loss scale already at minimum - cannot decrease scale anymore. Exiting run.")
+        self.cur_scale = max(self.cur_scale / self.scale_factor, self.min_scale)
+
     def update_scale(self, overflow):
+        """One optimizer step's verdict. An overflow first spends the hysteresis budget (`delayed_shift` - 1 free
+        passes), then divides the scale; `scale_window` steps since the last overflow multiply it back. The budget
+        refills on every clean step (`consecutive_hysteresis`) or only when the scale grows."""
+        step = self.cur_iter
+        self.cur_iter = step + 1
         if overflow:
-            if self.delayed_shift == 1 or self.cur_hysteresis == 1:
-                if self.cur_scale == self.min_scale and self.raise_error_at_min_scale:
-                    raise Exception("Current loss scale already at minimum - cannot decrease scale anymore. "
-                                    "Exiting run.")
-                self.cur_scale = max(self.cur_scale / self.scale_factor, self.min_scale)
-            else:
+            self.last_overflow_iter = step
+            if self.delayed_shift > 1 and self.cur_hysteresis > 1:
                 self.cur_hysteresis -= 1
-            self.last_overflow_iter = self.cur_iter
-        else:
-            if self.consecutive_hysteresis:
+            else:
+                self._shrink()
+            return
+        if self.consecutive_hysteresis:
+            self.cur_hysteresis = self.delayed_shift
+        if (step - self.last_overflow_iter) % self.scale_window == 0:
+            if not self.consecutive_hysteresis:
                 self.cur_hysteresis = self.delayed_shift
-            if (self.cur_iter - self.last_overflow_iter) % self.scale_window == 0:
-                if not self.consecutive_hysteresis:
-                    self.cur_hysteresis = self.delayed_shift
-                self.cur_scale *= self.scale_factor
-        self.cur_iter += 1
+            self.cur_scale *= self.scale_factor
 
 
 def CreateLossScaler(dtype, static_loss_scale, dynamic_scaling, dynamic_loss_args):
