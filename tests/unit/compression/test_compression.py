@@ -261,3 +261,38 @@ def test_tensor_parallel_compress_layers(tmp_path):
     ref.sum().backward()
     torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(gx, x.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_memory_efficient_linear_patch_skips_layers_with_their_own_forward():
+    """The engine routes plain `nn.Linear` layers through its memory-efficient linear function; compression layers
+    (and any other subclass with its own forward) must keep theirs, or masks / in-forward quantisation / the
+    tensor-parallel reductions inside them would silently stop applying."""
+    from deepspeedsyclsupport_amd.runtime.zero.linear import install_zero3_linear
+
+    class Scaled(nn.Linear):
+
+        def forward(self, x):
+            return super().forward(x) * 2.0
+
+    m = MLP()
+    cfg = _cfg(weight_quantization={"shared_parameters": {"enabled": True, "quantize_weight_in_forward": True,
+                                                          "quantize_groups": 1, "schedule_offset": 0},
+                                    "different_groups": {"wq": {"params": {"start_bits": 4, "target_bits": 4,
+                                                                           "quantization_period": 1},
+                                                                "modules": ["layers.0.*"]}}})
+    init_compression(m, cfg)
+    m.extra = Scaled(16, 16)
+    x = torch.randn(8, 16)
+    before = m(x)
+    ex_before = m.extra(x)
+    n = install_zero3_linear(m)
+    comp = [mod for mod in m.modules() if isinstance(mod, LinearLayer_Compress)]
+    plain = [mod for mod in m.modules() if type(mod) is nn.Linear]
+    assert comp and plain and n == len(plain)
+    assert all(not getattr(c, "_ds_zero3_linear", False) for c in comp) and not getattr(m.extra, "_ds_zero3_linear", False)
+    assert all(getattr(p, "_ds_zero3_linear", False) for p in plain)
+    torch.testing.assert_close(m(x), before)          # quantised-in-forward layers still quantise
+    torch.testing.assert_close(m.extra(x), ex_before)
+    lin = comp[0]
+    assert not torch.allclose(lin(x), nn.functional.linear(x, lin.weight, lin.bias))  # i.e. its own forward ran
+    assert install_zero3_linear(m) == 0               # idempotent
