@@ -280,24 +280,32 @@ class DSInferenceLayer(nn.Module):
         if isinstance(meta, RaggedMeta):
             return self._attend_ragged(qkv, meta, cache, rope, alibi)
         spec = self.spec
-        B, n, D = qkv.shape[0], meta.n_new, spec.head_dim
+        pending = qkv if hasattr(qkv, "finalize_rms") else None  # un-finalized weight-only GEMV (PendingAcc)
+        if pending is not None and not (pending.acc.is_cuda and cache.k[self.layer_idx].dtype == torch.bfloat16):
+            qkv, pending = pending.finalize(), None
+        B, n, D = (pending.lead[0] if pending is not None else qkv.shape[0]), meta.n_new, spec.head_dim
         kc, vc = cache.k[self.layer_idx], cache.v[self.layer_idx]
         k = v = None
         scale = spec.attn_scale or 1.0 / math.sqrt(D)
         window = spec.layer_windows[self.layer_idx] if spec.layer_windows else spec.sliding_window
         # ALiBi / windowed prompts and chunk continuations: ragged paged flash prefill over the cache
         # (head dims other than 128 always take it: the dense flash forward is a 128-wide kernel)
-        paged = n > 1 and D in PAGED_HEAD_DIMS and qkv.is_cuda and qkv.dtype == torch.bfloat16 \
+        paged = n > 1 and D in PAGED_HEAD_DIMS and (pending is not None or (qkv.is_cuda and
+                                                                             qkv.dtype == torch.bfloat16)) \
             and kc.dtype == torch.bfloat16 and (not meta.prefill_from_zero or alibi is not None or bool(window)
                                                 or D != 128)
-        if qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16:
-            # one fused HIP epilogue: split + RoPE(q, k) + scatter k/v into the paged cache
+        if pending is not None or (qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16):
+            # one fused HIP epilogue: split + RoPE(q, k) + scatter k/v into the paged cache (and, for a pending
+            # weight-only GEMV, its finalize pass: the sums are read straight from the split-K workspace)
             from ...ops.native import hip_ops
             rot = spec.rotary_dim if spec.pos in ("rope", "rope_gptj") else 0
             want_kv = meta.prefill_from_zero and n > 1 and not paged
-            outs = hip_ops().qkv_rope_append(qkv.contiguous(), rope[0] if rot else None, rope[1] if rot else None,
+            src = pending._take() if pending is not None else qkv.contiguous()
+            outs = hip_ops().qkv_rope_append(src, rope[0] if rot else None, rope[1] if rot else None,
                                              meta.pos_ids, kc, vc, meta.block_tables, meta.start_pos, n, self.hq,
-                                             self.hk, rot, spec.pos == "rope_gptj", want_kv)
+                                             self.hk, rot, spec.pos == "rope_gptj", want_kv, None,
+                                             pending.M if pending is not None else 0,
+                                             pending.bias if pending is not None else None)
             q = outs[0].view(B, n, self.hq, D)
             if want_kv:
                 k, v = outs[1].view(B, n, self.hk, D), outs[2].view(B, n, self.hk, D)
@@ -331,11 +339,17 @@ class DSInferenceLayer(nn.Module):
         kc, vc = cache.k[self.layer_idx], cache.v[self.layer_idx]
         rot = spec.rotary_dim if spec.pos in ("rope", "rope_gptj") else 0
         inter = spec.pos == "rope_gptj"
-        if qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16:
+        pending = qkv if hasattr(qkv, "finalize_rms") else None
+        if pending is not None and not (pending.acc.is_cuda and kc.dtype == torch.bfloat16):
+            qkv, pending = pending.finalize(), None
+        if pending is not None or (qkv.is_cuda and qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16):
             from ...ops.native import hip_ops
-            q = hip_ops().qkv_rope_append(qkv.reshape(T, -1).contiguous(), rope[0] if rot else None,
+            src = pending._take() if pending is not None else qkv.reshape(T, -1).contiguous()
+            q = hip_ops().qkv_rope_append(src, rope[0] if rot else None,
                                           rope[1] if rot else None, meta.pos_ids, kc, vc, meta.block_tables,
-                                          meta.start_pos, 1, self.hq, self.hk, rot, inter, False, meta.seq_ids)[0]
+                                          meta.start_pos, 1, self.hq, self.hk, rot, inter, False, meta.seq_ids,
+                                          pending.M if pending is not None else 0,
+                                          pending.bias if pending is not None else None)[0]
         else:
             q, k, v = qkv.reshape(1, T, self.hq + 2 * self.hk, D).split([self.hq, self.hk, self.hk], dim=2)
             q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
@@ -444,9 +458,9 @@ class DSInferenceLayer(nn.Module):
     def _forward_quant_skinny(self, h, residual, meta, cache, rope, alibi):
         """Decode (<= 16 token rows) over int8 / int4 weights: the four weight streams leave their sums in the fp32
         split-K workspace and the op that consumes each projection anyway — residual add + RMSNorm after the
-        attention-output and MLP-down projections, the gated activation after gate/up — converts and re-zeroes it
-        (`csrc/gemv/skinny_finalize.hip`). The block output is returned still pending: the next layer's input norm
-        consumes it. 8 launches per layer instead of 14."""
+        attention-output and MLP-down projections, the gated activation after gate/up, the RoPE + cache-append
+        epilogue after QKV — converts and re-zeroes it (`csrc/gemv/skinny_finalize.hip`, `csrc/attn/decode_attn.hip`).
+        The block output is returned still pending: the next layer's input norm consumes it."""
         from ...ops.int8_gemv import PendingAcc
         from ...ops.transformer.functional import ACT_CODES
         eps, q = self.spec.norm_eps, self.quant
@@ -456,8 +470,8 @@ class DSInferenceLayer(nn.Module):
             normed, res1 = self._norm(h, self.ln1_w, None), h
         else:
             normed, res1 = self._norm(h, self.ln1_w, None, residual)
-        qkv = q["qkv_w"].i8.linear(normed, self.qkv_b)
-        attn = self._attend(qkv, meta, cache, rope, alibi)
+        # the fused QKV epilogue (RoPE + cache append) consumes the projection's sums straight from the workspace
+        attn = self._attend(q["qkv_w"].i8.raw(normed, self.qkv_b), meta, cache, rope, alibi)
         normed2, res2 = q["o_w"].i8.raw(attn, self.o_b).finalize_rms(res1, self.ln2_w, eps)
         up = q["fc1_w"].i8.raw(normed2, self.fc1_b)
         if self.spec.gated_mlp:

@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(256) qkv_rope_append_kernel(
     const int* __restrict__ pos, bf16* __restrict__ q_out, bf16* __restrict__ k_out, bf16* __restrict__ v_out,
     bf16* __restrict__ kc, bf16* __restrict__ vc, const int* __restrict__ block_table,
     const int* __restrict__ start_pos, const int* __restrict__ seq_ids, int n_new, int Hq, int Hk, int D, int rot,
-    int interleaved, int BS, int max_blocks) {
+    int interleaved, int BS, int max_blocks, float* __restrict__ acc, const bf16* __restrict__ acc_bias, int NP) {
   // grid = (tokens, head groups): 256 threads cover 256 / (D/2) heads of one token, one thread per element pair
   const int H3 = Hq + 2 * Hk, half = D / 2, rh = rot / 2;
   const int tph = half < (int)blockDim.x ? half : (int)blockDim.x;
@@ -246,9 +246,21 @@ __global__ void __launch_bounds__(256) qkv_rope_append_kernel(
   // cache slot = its position
   const int t = blockIdx.x, h = blockIdx.y * (blockDim.x / tph) + threadIdx.x / tph;
   const int b = seq_ids ? seq_ids[t] : t / n_new, j = seq_ids ? 0 : t % n_new;
+  // acc != null: the fused projection's sums still sit in the weight-only GEMV's fp32 split-K workspace [rows, NP]
+  // (skinny_int8.hip / skinny_int4.hip without their finalize pass): read them (+ bias) from there and re-zero what
+  // was read, padding columns included, so this kernel IS that GEMV's finalize pass
+  float* arow = acc ? acc + (int64_t)t * NP : nullptr;
+  if (arow && blockIdx.y == 0)
+    for (int i = H3 * D + threadIdx.x; i < NP; i += blockDim.x) arow[i] = 0.f;
   // (head dims whose half does not divide the block leave a few surplus threads at the end)
   if (h >= H3 || (int)threadIdx.x / tph >= (int)blockDim.x / tph) return;
-  const bf16* src = qkv + ((int64_t)t * H3 + h) * D;
+  const bf16* src = acc ? nullptr : qkv + ((int64_t)t * H3 + h) * D;
+  auto ld = [&](int d) -> float {
+    if (arow == nullptr) return (float)src[d];
+    const float v = arow[h * D + d] + (acc_bias ? (float)acc_bias[h * D + d] : 0.f);
+    arow[h * D + d] = 0.f;
+    return (float)(bf16)v;  // the unfused path rounds the projection to bf16 before RoPE
+  };
   bf16* dst;
   bf16* extra = nullptr;
   if (h < Hq) {
@@ -271,7 +283,7 @@ __global__ void __launch_bounds__(256) qkv_rope_append_kernel(
       d0 = rot + 2 * (i - rh);
       d1 = d0 + 1;
     }
-    float a = (float)src[d0], c = (float)src[d1];
+    float a = ld(d0), c = ld(d1);
     if (i < rh && h < Hq + Hk) {
       const float cs = cosT[(int64_t)p * rh + i], sn = sinT[(int64_t)p * rh + i];
       const float a2 = a * cs - c * sn;
@@ -341,12 +353,15 @@ extern "C" int ds_kv_append(const void* k, const void* v, void* kc, void* vc, co
 extern "C" int ds_qkv_rope_append(const void* qkv, const float* cosT, const float* sinT, const int* pos, void* q_out,
                                   void* k_out, void* v_out, void* kc, void* vc, const int* block_table,
                                   const int* start_pos, const int* seq_ids, int T, int n_new, int Hq, int Hk, int D,
-                                  int rot, int interleaved, int BS, int max_blocks, hipStream_t s) {
+                                  int rot, int interleaved, int BS, int max_blocks, float* acc, const void* acc_bias,
+                                  int NP, hipStream_t s) {
   if (D % 2 || rot % 2 || rot > D || (D - rot) % 2 || T <= 0) return T == 0 ? 0 : (int)hipErrorInvalidValue;
+  if (acc != nullptr && (NP < (Hq + 2 * Hk) * D || T > 16)) return (int)hipErrorInvalidValue;
+  if (acc == nullptr && qkv == nullptr) return (int)hipErrorInvalidValue;
   const int tph = D / 2 < 256 ? D / 2 : 256, hpb = 256 / tph;
   hipLaunchKernelGGL(qkv_rope_append_kernel, dim3(T, (Hq + 2 * Hk + hpb - 1) / hpb), dim3(256), 0, s, (const bf16*)qkv, cosT, sinT, pos,
                      (bf16*)q_out, (bf16*)k_out, (bf16*)v_out, (bf16*)kc, (bf16*)vc, block_table, start_pos, seq_ids,
-                     n_new, Hq, Hk, D, rot, interleaved, BS, max_blocks);
+                     n_new, Hq, Hk, D, rot, interleaved, BS, max_blocks, acc, (const bf16*)acc_bias, NP);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -18,7 +18,8 @@ int ds_skinny_mfma(const void*, const void*, const void*, const void*, const voi
                    int, int, int, int, float, hipStream_t);
 int ds_rms_fwd(const void*, const void*, const void*, void*, void*, float*, int64_t, int, float, int, hipStream_t);
 int ds_qkv_rope_append(const void*, const float*, const float*, const int*, void*, void*, void*, void*, void*,
-                       const int*, const int*, const int*, int, int, int, int, int, int, int, int, int, hipStream_t);
+                       const int*, const int*, const int*, int, int, int, int, int, int, int, int, int, float*,
+                       const void*, int, hipStream_t);
 int ds_paged_prefill(const void*, const void*, const void*, void*, const int*, const int*, const int*, const int*, int,
                      const float*, int, int, int, int, int, int, float, hipStream_t);
 int ds_paged_decode(const void*, const void*, const void*, const int*, const int*, const float*, float*, float*, void*,
@@ -209,35 +210,52 @@ Tensor skinny_gemm(Tensor x, Tensor w, OptT bias, OptT add, int64_t in_mode, boo
 }
 
 // qkv [T, (Hq+2Hk)*D] -> q [T, Hq, D] roped; k (roped) / v scattered into the paged cache; optional k/v copies.
+// `qkv` is either the bf16 projection or — with `acc_rows` > 0 — the fp32 workspace view [16, NP] a weight-only GEMV left
+// un-finalized (skinny_q_raw): then the kernel adds `acc_bias`, and re-zeroes the workspace rows it consumed.
 std::vector<Tensor> qkv_rope_append(Tensor qkv, OptT cos, OptT sin, Tensor pos, Tensor kc, Tensor vc,
                                     Tensor block_table, Tensor start_pos, int64_t n_new, int64_t Hq, int64_t Hk,
-                                    int64_t rot, bool interleaved, bool want_kv, OptT seq_ids) {
+                                    int64_t rot, bool interleaved, bool want_kv, OptT seq_ids, int64_t acc_rows,
+                                    OptT acc_bias) {
   need(qkv, "qkv"); need(pos, "pos"); need(kc, "kc"); need(vc, "vc"); need(block_table, "block_table");
   need(start_pos, "start_pos");
-  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && kc.scalar_type() == at::kBFloat16, "bf16 qkv / cache");
+  const bool from_acc = acc_rows > 0;
+  TORCH_CHECK(kc.scalar_type() == at::kBFloat16 && (from_acc ? qkv.scalar_type() == at::kFloat
+                                                             : qkv.scalar_type() == at::kBFloat16),
+              "bf16 qkv (or fp32 GEMV workspace) / bf16 cache");
   const int D = (int)kc.size(3);
-  const int64_t T = qkv.numel() / ((Hq + 2 * Hk) * D);
+  const int64_t N3 = (Hq + 2 * Hk) * D;
+  const int64_t T = from_acc ? acc_rows : qkv.numel() / N3;
   const bool ragged = seq_ids.has_value() && seq_ids->defined();
-  TORCH_CHECK(T * (Hq + 2 * Hk) * D == qkv.numel() && (ragged || T % n_new == 0), "qkv shape");
+  if (from_acc)
+    TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == 16 && qkv.size(1) >= N3 && T <= 16, "workspace view [16, NP >= N]");
+  TORCH_CHECK((from_acc || T * N3 == qkv.numel()) && (ragged || T % n_new == 0), "qkv shape");
+  const void* abp = nullptr;
+  if (from_acc && acc_bias.has_value() && acc_bias->defined()) {
+    need(*acc_bias, "acc_bias");
+    TORCH_CHECK(acc_bias->scalar_type() == at::kBFloat16 && acc_bias->numel() == N3, "acc_bias bf16 [N]");
+    abp = acc_bias->data_ptr();
+  }
   if (ragged) {
     need(*seq_ids, "seq_ids");
     TORCH_CHECK(seq_ids->scalar_type() == at::kInt && seq_ids->numel() == T && pos.numel() == T, "seq_ids / pos [T]");
   }
   TORCH_CHECK(kc.size(1) == Hk, "cache kv heads");
   TORCH_CHECK(rot == 0 || (cos.has_value() && sin.has_value()), "rope tables required");
-  auto q = torch::empty({T, Hq, D}, qkv.options());
+  auto bopt = kc.options();
+  auto q = torch::empty({T, Hq, D}, bopt);
   Tensor k, v;
   if (want_kv) {
-    k = torch::empty({T, Hk, D}, qkv.options());
-    v = torch::empty({T, Hk, D}, qkv.options());
+    k = torch::empty({T, Hk, D}, bopt);
+    v = torch::empty({T, Hk, D}, bopt);
   }
-  check(ds_qkv_rope_append(qkv.data_ptr(), rot ? cos->data_ptr<float>() : nullptr,
+  check(ds_qkv_rope_append(from_acc ? nullptr : qkv.data_ptr(), rot ? cos->data_ptr<float>() : nullptr,
                            rot ? sin->data_ptr<float>() : nullptr, pos.data_ptr<int>(), q.data_ptr(),
                            want_kv ? k.data_ptr() : nullptr, want_kv ? v.data_ptr() : nullptr, kc.data_ptr(),
                            vc.data_ptr(), block_table.data_ptr<int>(), start_pos.data_ptr<int>(),
                            ragged ? seq_ids->data_ptr<int>() : nullptr, (int)T, (int)n_new,
                            (int)Hq, (int)Hk, D, (int)rot, interleaved ? 1 : 0, (int)kc.size(2),
-                           (int)block_table.size(1), stream()),
+                           (int)block_table.size(1), from_acc ? qkv.data_ptr<float>() : nullptr, abp,
+                           from_acc ? (int)qkv.size(1) : 0, stream()),
         "qkv_rope_append");
   if (want_kv) return {q, k, v};
   return {q};
@@ -499,7 +517,8 @@ void register_inference_ops(pybind11::module& m) {
   m.def("skinny_set_path", &skinny_set_path);
   m.def("qkv_rope_append", &qkv_rope_append, py::arg("qkv"), py::arg("cos"), py::arg("sin"), py::arg("pos"),
         py::arg("kc"), py::arg("vc"), py::arg("block_table"), py::arg("start_pos"), py::arg("n_new"), py::arg("Hq"),
-        py::arg("Hk"), py::arg("rot"), py::arg("interleaved"), py::arg("want_kv"), py::arg("seq_ids") = py::none());
+        py::arg("Hk"), py::arg("rot"), py::arg("interleaved"), py::arg("want_kv"), py::arg("seq_ids") = py::none(), py::arg("acc_rows") = 0,
+        py::arg("acc_bias") = py::none());
   m.def("paged_decode", &paged_decode);
   m.def("kv_append", &kv_append);
   m.def("quantize", &quantize);

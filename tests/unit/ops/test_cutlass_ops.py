@@ -50,8 +50,10 @@ def test_moe_gemm_cpu():
 
 
 def test_builder_is_honest():
+    """int8 and int4 have native kernels; anything else (e.g. FP6) is reported as not available."""
     b = InferenceCutlassBuilder()
-    assert not b.is_compatible(num_bits=4)
+    assert b.is_compatible(num_bits=4) == b.is_compatible(num_bits=8)
+    assert not b.is_compatible(num_bits=6)
     assert "cutlass_ops" in ALL_OPS and "evoformer_attn" in ALL_OPS
 
 
