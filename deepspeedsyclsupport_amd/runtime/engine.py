@@ -101,7 +101,7 @@ class DeepSpeedEngine(nn.Module):
         self._configure_checkpointing()
         self._configure_data_efficiency()
         self._configure_autotuning()
-        if self.global_rank == 0 and self._config.param_dict.get("print_config", False):
+        if self.global_rank == 0 and (self._config.dump_state or self._config.param_dict.get("print_config", False)):
             self._config.print("DeepSpeedEngine configuration")
 
     # ============================================================================================ data efficiency
@@ -350,6 +350,7 @@ class DeepSpeedEngine(nn.Module):
         stage = self.zero_optimization_stage()
         dtype = self._dtype()
         zc = self._config.zero_config
+        self._check_optimizer_options(basic, stage, zc)
         if getattr(zc, "memory_efficient_linear", True) and next(self.module.parameters()).is_cuda:
             # every nn.Linear on the training linear of ops/linear.py (K-major weight-gradient GEMMs; the ZeRO-3
             # coordinator installs the same function for partitioned runs)
@@ -377,6 +378,57 @@ class DeepSpeedEngine(nn.Module):
                                            gradient_accumulation_steps=self.gradient_accumulation_steps(),
                                            sparse_params=sparse_params)
 
+    def _check_optimizer_options(self, basic, stage, zc):
+        """Config keys that gate optimizer choices (reference `runtime/engine.py:1219-1265,1475-1500`): an optimizer
+        ZeRO was not validated with needs `zero_allow_untested_optimizer`. Optimizer offload steps the host partitions
+        with the native CPU Adam, so a client `torch.optim.Adam` / `AdamW` / `DeepSpeedCPUAdam` is taken over by the
+        flat Adam path (same update rule, hyper-parameters read from its param groups) and any other optimizer is
+        refused up front, whatever `zero_force_ds_cpu_optimizer` says: there is no torch fallback for host shards."""
+        from ..ops.adagrad.cpu_adagrad import DeepSpeedCPUAdagrad
+        from ..ops.adam.cpu_adam import DeepSpeedCPUAdam
+        from ..ops.adam.fused_adam import FusedAdam
+        from ..ops.lamb.fused_lamb import FusedLamb
+        from ..ops.lion.cpu_lion import DeepSpeedCPULion
+        from ..ops.lion.fused_lion import FusedLion
+        from .zero.utils import ZeRORuntimeException
+        cfg = self._config
+        flat_adam = isinstance(basic, FusedAdam) or getattr(basic, "_ds_flat_adam", False)
+        tested = (torch.optim.Adam, torch.optim.AdamW, FusedAdam, DeepSpeedCPUAdam, DeepSpeedCPUAdagrad,
+                  DeepSpeedCPULion, FusedLion, FusedLamb, torch.optim.Adagrad)
+        if stage > 0 and not isinstance(basic, tested) and not flat_adam and not cfg.zero_allow_untested_optimizer:
+            raise ZeRORuntimeException(
+                f"You are using an untested ZeRO Optimizer ({type(basic).__name__}). Please add "
+                f"<\"zero_allow_untested_optimizer\": true> in the configuration file to use it.")
+        off = getattr(zc, "offload_optimizer", None)
+        offloading = off is not None and str(getattr(off.device, "value", off.device)) in ("cpu", "nvme")
+        if offloading and not flat_adam:
+            plain = all(not g.get(k, False) for g in basic.param_groups for k in ("amsgrad", "maximize"))
+            if isinstance(basic, DeepSpeedCPUAdam):
+                basic._ds_flat_adam = True  # already carries adam_w_mode
+            elif isinstance(basic, torch.optim.AdamW) and plain:
+                basic._ds_flat_adam, basic.adam_w_mode = True, True
+            elif isinstance(basic, torch.optim.Adam) and plain:
+                basic._ds_flat_adam, basic.adam_w_mode = True, False
+            else:
+                hint = "" if cfg.zero_force_ds_cpu_optimizer else \
+                    " (zero_force_ds_cpu_optimizer=false does not help: host shards have no torch-stepped fallback)"
+                raise ZeRORuntimeException(
+                    f"optimizer offload steps the host partitions with the native CPU Adam; "
+                    f"{type(basic).__name__} cannot be offloaded. Use Adam / AdamW / DeepSpeedCPUAdam{hint}.")
+        if cfg.fp16_master_weights_and_gradients:
+            raise NotImplementedError("fp16.fp16_master_weights_and_grads: master weights are kept in fp32 (or as a "
+                                      "bf16 weight + 16-bit residual with bf16.split_master_weights)")
+        if cfg.mics_hierarchial_params_gather:
+            log_dist("mics_hierarchical_params_gather: MiCS shard groups are laid inside one xGMI node, where a single "
+                     "all-gather already uses every link; the two-level gather is not used", ranks=[0])
+        if cfg.graph_harvesting:
+            log_dist("graph_harvesting: the gradient-norm and clipping passes are already single multi-tensor "
+                     "launches (sumsq_multi, clip folded into the Adam kernel's gradient scale); nothing to capture",
+                     ranks=[0])
+        if cfg.bfloat16_immediate_grad_update:
+            log_dist("bf16.immediate_grad_update: gradients are always folded into the flat reduction buffers from "
+                     "the backward hooks (the immediate form)", ranks=[0])
+
     def _configure_lr_scheduler(self, client_lr_scheduler):
         name = self._config.scheduler_name
         if name is not None:
@@ -391,8 +443,11 @@ class DeepSpeedEngine(nn.Module):
     def _configure_checkpointing(self):
         self.checkpoint_engine = AsyncCheckpointEngine() if self._config.nebula_config.get("enabled", False) \
             else TorchCheckpointEngine()
-        self.save_non_zero_checkpoint = dist.get_rank(self.seq_data_parallel_group) == 0 or \
-            self.zero_optimization_stage() == 3
+        # `checkpoint.use_node_local_storage` (reference `runtime/engine.py:933-941,3070`): every node has its own
+        # disk, so local rank 0 of EVERY node writes the model file, creates the folder and the `latest` marker
+        self._ckpt_lead_rank = self.local_rank if self._config.use_node_local_storage else dist.get_rank()
+        lead = self.local_rank if self._config.use_node_local_storage else dist.get_rank(self.seq_data_parallel_group)
+        self.save_non_zero_checkpoint = lead == 0 or self.zero_optimization_stage() == 3
         self.save_zero_checkpoint = self.optimizer is not None
 
     # ============================================================================================ config accessors
@@ -550,9 +605,26 @@ class DeepSpeedEngine(nn.Module):
             kwargs.update(self.progressive_layer_drop.get_state())
         if self.optimizer is not None:
             self.optimizer.offload_pre_forward()
+        if self._config.fp16_auto_cast:
+            # reference `runtime/engine.py:1808-1810`: floating-point inputs follow the fp16 module
+            inputs = self._cast_inputs_half(inputs)
+            kwargs = self._cast_inputs_half(kwargs)
         loss = self.module(*inputs, **kwargs)
         self.timers(FORWARD_MICRO_TIMER).stop()
         return loss
+
+    @staticmethod
+    def _cast_inputs_half(inputs):
+        """Floating-point tensors anywhere inside tuples / lists / dicts become fp16 (reference
+        `runtime/engine.py:1757-1772`)."""
+        cast = DeepSpeedEngine._cast_inputs_half
+        if isinstance(inputs, (list, tuple)):
+            return type(inputs)(cast(v) for v in inputs)
+        if isinstance(inputs, dict):
+            return {k: cast(v) for k, v in inputs.items()}
+        if torch.is_tensor(inputs) and inputs.is_floating_point():
+            return inputs.half()
+        return inputs
 
     def _scale_loss_by_gas(self, loss):
         gas = self.gradient_accumulation_steps()
@@ -812,12 +884,13 @@ class DeepSpeedEngine(nn.Module):
             tag = f"global_step{self.global_steps}"
         tag = str(tag)
         self._checkpoint_tag_validation(tag)
-        if dist.get_rank() == 0:
+        if self._ckpt_lead_rank == 0:
             os.makedirs(os.path.join(save_dir, tag), exist_ok=True)
         dist.barrier()
         os.makedirs(os.path.join(save_dir, tag), exist_ok=True)
+        self._curr_ckpt_path = os.path.join(save_dir, tag)
         module_sd = self.module_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
-        if getattr(self, "has_moe_layers", False):
+        if getattr(self, "has_moe_layers", False) and module_sd is not None:
             self._save_moe_experts(save_dir, tag, module_sd)
         zero = self.optimizer is not None
         sampler = None
@@ -850,13 +923,13 @@ class DeepSpeedEngine(nn.Module):
             osd = self.optimizer.state_dict()
             zsd = dict(optimizer_state_dict=osd, ds_config=self._config.param_dict, ds_version=_version())
             self.checkpoint_engine.save(zsd, self._get_zero_ckpt_name(save_dir, tag))
-            if dist.get_rank() == 0:
+            if self._ckpt_lead_rank == 0:
                 self._copy_recovery_script(save_dir)
         self.checkpoint_engine.commit(tag)
         dist.barrier()
         if zero and getattr(self._config.checkpoint_config, "write_reference_format", False):
             self._write_reference_format(save_dir, tag)
-        if save_latest and dist.get_rank() == 0:
+        if save_latest and self._ckpt_lead_rank == 0:
             with open(os.path.join(save_dir, "latest"), "w") as f:
                 f.write(tag)
         dist.barrier()
@@ -897,12 +970,14 @@ class DeepSpeedEngine(nn.Module):
         if not os.path.exists(path):
             # different topology: any model-states file carries the replicated metadata (and, outside ZeRO-3, the
             # full module)
-            cands = sorted(f for f in os.listdir(tag_dir) if f.endswith(CK.MODEL_FILE_SUFFIX) and "expert_" not in f)
+            cands = sorted(f for f in os.listdir(tag_dir) if f.endswith(CK.MODEL_FILE_SUFFIX) and
+                           not f.startswith(CK.LAYER_FILE_PREFIX))  # (layer_* = expert and pipeline-layer files)
             if not cands:
                 raise FileNotFoundError(f"no model-states file in {tag_dir}")
             path = os.path.join(tag_dir, cands[0])
         ck = self.checkpoint_engine.load(path, map_location="cpu")
         module_sd = dict(ck.get("module") or {})
+        self._curr_ckpt_path = tag_dir
         if getattr(self, "has_moe_layers", False):
             self._load_moe_experts(load_dir, tag, module_sd)
         placeholders = self._load_module_state(module_sd, strict=load_module_strict)

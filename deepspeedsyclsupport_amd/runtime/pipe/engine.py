@@ -48,8 +48,41 @@ class PipelineEngine(DeepSpeedEngine):
         self.loss = torch.tensor(0.0, device=self.device)
         self.data_iterator = None
         self.batch_fn = None
+        self.module.checkpoint_parallel_write_pipeline = self._config.checkpoint_parallel_write_pipeline
         log_dist(f"PipelineEngine: stages={self.num_stages} stage={self.stage_id} dp={self.grid.data_parallel_size} "
                  f"micro_batches={self.micro_batches}", ranks=[-1])
+
+    # ------------------------------------------------------------------------------------------ checkpoints
+    def module_state_dict(self, destination=None, prefix="", keep_vars=False, exclude_frozen_parameters=False):
+        """The stage's weights go to one file per layer, indexed by global layer number, next to the per-stage
+        model-states file, which then carries no module (reference `runtime/pipe/engine.py:1324-1345`): that is what
+        lets a checkpoint load under another stage count. Returns the plain dict only outside a checkpoint save."""
+        path = getattr(self, "_curr_ckpt_path", None)
+        if path is None:
+            return super().module_state_dict(destination, prefix, keep_vars, exclude_frozen_parameters)
+        self.module.save_state_dict(path, self.checkpoint_engine, exclude_frozen_params=exclude_frozen_parameters)
+        return None
+
+    def save_checkpoint(self, *args, **kwargs):
+        try:
+            return super().save_checkpoint(*args, **kwargs)
+        finally:
+            self._curr_ckpt_path = None
+
+    def load_checkpoint(self, *args, **kwargs):
+        try:
+            return super().load_checkpoint(*args, **kwargs)
+        finally:
+            self._curr_ckpt_path = None
+
+    @torch.no_grad()
+    def _load_module_state(self, sd, strict=True):
+        if sd:  # a checkpoint that carries the module inline
+            return super()._load_module_state(sd, strict=strict)
+        self.module.load_state_dir(self._curr_ckpt_path, self.checkpoint_engine, strict=strict)
+        if self.optimizer is not None:
+            self.optimizer.refresh_from_module()
+        return []
 
     # ------------------------------------------------------------------------------------------ helpers
     def is_first_stage(self):

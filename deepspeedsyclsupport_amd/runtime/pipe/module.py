@@ -142,6 +142,9 @@ class PipelineModule(nn.Module):
             from ..activation_checkpointing import checkpointing
             activation_checkpoint_func = checkpointing.checkpoint
         self.activation_checkpoint_func = activation_checkpoint_func
+        # layer files written by every data-parallel replica (an even share each) instead of replica 0 alone; the
+        # pipeline engine sets it from checkpoint.parallel_write.pipeline_stage
+        self.checkpoint_parallel_write_pipeline = False
 
     # ------------------------------------------------------------------------------------------ partitioning
     def _stage_boundaries(self, method):
@@ -287,3 +290,57 @@ class PipelineModule(nn.Module):
         idx = local_layer_idx + self._local_start
         suffix = self._grid._topo.get_rank_repr(rank=self.global_rank)
         return os.path.join(ckpt_dir, f"layer_{idx:02d}" + (f"-{suffix}" if suffix else "") + "-model_states.pt")
+
+    def ckpt_layer_path_list(self, ckpt_dir, local_layer_idx):
+        """Every model-slice file of one layer, sorted (one per tensor-parallel rank of the saving run)."""
+        import glob
+        idx = local_layer_idx + self._local_start
+        return sorted(glob.glob(os.path.join(ckpt_dir, f"layer_{idx:02d}-*model_states.pt")))
+
+    def _frozen_names(self, layer):
+        return [n for n, p in layer.named_parameters() if not p.requires_grad]
+
+    def save_state_dict(self, save_dir, checkpoint_engine, exclude_frozen_params=False):
+        """One `layer_XX-model_YY-model_states.pt` per local layer (reference `runtime/pipe/module.py:567-598`): the
+        files are indexed by GLOBAL layer number, so a checkpoint loads under any stage count. Replicas hold the same
+        weights: replica 0 writes them all, or, with `checkpoint_parallel_write_pipeline`, each replica an even share
+        (all 7 xGMI peers of a node writing at once instead of one)."""
+        from ...checkpoint.utils import clone_tensors_for_torch_save
+        dp_rank, dp_size = self._grid.data_parallel_id, self._grid.data_parallel_size
+        n = len(self.forward_funcs)
+        if self.checkpoint_parallel_write_pipeline:
+            cuts = partition_uniform(n, dp_size)
+            start, end = cuts[dp_rank], cuts[dp_rank + 1]
+        elif dp_rank != 0:
+            return
+        else:
+            start, end = 0, n
+        checkpoint_engine.makedirs(save_dir, exist_ok=True)
+        for i in range(start, end):
+            layer = self.forward_funcs[i]
+            if not hasattr(layer, "state_dict"):
+                continue
+            sd = layer.state_dict()
+            if exclude_frozen_params:
+                for name in self._frozen_names(layer):
+                    del sd[name]
+            checkpoint_engine.save(clone_tensors_for_torch_save(sd), self.ckpt_layer_path(save_dir, i))
+
+    def load_state_dir(self, load_dir, checkpoint_engine, strict=True):
+        """Inverse of `save_state_dict` (reference `runtime/pipe/module.py:600-625`): every local layer reads its
+        file(s); a different tensor-parallel degree merges or splits them through the Megatron state-dict loader."""
+        from ..state_dict_factory import SDLoaderFactory
+        mp_rank = self._grid.get_slice_parallel_rank()
+        mp_size = self._grid.get_slice_parallel_world_size()
+        for i, layer in enumerate(self.forward_funcs):
+            if not hasattr(layer, "load_state_dict"):
+                continue
+            files = self.ckpt_layer_path_list(load_dir, i)
+            if not files:
+                if strict:
+                    raise FileNotFoundError(f"no checkpoint file for layer {i + self._local_start} in {load_dir}")
+                continue
+            loader = SDLoaderFactory.get_sd_loader(files, version=2.0, checkpoint_engine=checkpoint_engine)
+            _, sd, _ = loader.load(mp_size, mp_rank, module_key=None, is_pipe_parallel=True)
+            layer.load_state_dict(sd, strict=strict)
+        self._synchronize_tied_weights()

@@ -205,19 +205,19 @@ class PipelineParallelGrid:
     def get_data_parallel_group(self):
         return self.dp_proc_group
 
+    # "model parallel" for the engine = everything that is not data parallel (pipe stages x tensor slices), as in the
+    # reference grid (`runtime/pipe/topology.py:436-443`): checkpoint file names and mp_world_size are built on it
     def get_model_parallel_rank(self):
-        if self.model_parallel_size == 1:
-            return self.ds_model_rank
-        return self._topo.get_coord(self.global_rank).model
+        return self.ds_model_rank
 
     def get_model_parallel_world_size(self):
-        return self.model_parallel_size
+        return self.ds_model_world_size
 
     def get_model_parallel_group(self):
-        return self.model_parallel_group
+        return self.ds_model_proc_group
 
     def get_slice_parallel_rank(self):
-        return self.get_model_parallel_rank() if "model" in self._topo.get_axis_names() else 0
+        return self._topo.get_coord(self.global_rank).model if "model" in self._topo.get_axis_names() else 0
 
     def get_slice_parallel_world_size(self):
         return self.slice_parallel_size

@@ -949,9 +949,19 @@ class FlatZeroOptimizer(ZeROOptimizer):
 
     def _post_step_gather(self):
         """Refresh full params of persistent groups from the updated shards (ZeRO-1/2, ZeRO-3 persistent)."""
+        no_allgather = bool(getattr(self.cfg, "disable_allgather", False))
         for g in self.groups:
             if g.partition and g.persistent and g.full is not None:
-                dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
+                if not no_allgather:
+                    dist.all_gather_into_tensor(g.full, g.shard, group=g.dp_group)
+                    continue
+                # `disable_allgather` (reference `runtime/config.py:270`): every owner broadcasts its segment instead
+                # (for fabrics or debug sessions where the all-gather is the suspect); same bytes, dp launches
+                for r in range(g.dp):
+                    piece = g.full[r * g.seg:(r + 1) * g.seg]
+                    if r == g.rank and piece.data_ptr() != g.shard.data_ptr():
+                        piece.copy_(g.shard)
+                    dist.broadcast(piece, dist.get_global_rank(g.dp_group, r), group=g.dp_group)
 
     def _zero_grad_buffers(self):
         for g in self.groups:

@@ -27,7 +27,7 @@ def _flags():
     pyinc = sysconfig.get_paths()["include"]
     pylib = sysconfig.get_config_var("LIBDIR")
     pyver = f"python{sys.version_info.major}.{sys.version_info.minor}"
-    cflags = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+    cflags = ["-std=c++17", "-O1", "-g", "-fopenmp", "-fno-omit-frame-pointer", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
               "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-deprecated-declarations"]
     cflags += [f"-isystem{p}" for p in inc] + [f"-isystem{pyinc}"]
     lflags = [f"-L{p}" for p in libs] + [f"-Wl,-rpath,{p}" for p in libs]

@@ -75,7 +75,8 @@ def _check_sparse(eng):
 
 @pytest.mark.parametrize("stage", [0, 1, 2, 3])
 def test_sparse_embedding_gradients(stage, tmp_path):
-    _same(tmp_path, stage, {"sparse_gradients": True}, _check_sparse)
+    # (rows summed after an all-gather vs inside a reduce-scatter: a different fp32 summation order)
+    _same(tmp_path, stage, {"sparse_gradients": True}, _check_sparse, atol=5e-6)
 
 
 def test_sparse_tensor_allreduce_roundtrip():
