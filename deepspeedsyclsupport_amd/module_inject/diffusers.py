@@ -115,12 +115,14 @@ class DSDiffusersAttention(nn.Module):
         if attention_mask is not None:
             B_, Nq = q.shape[0], q.shape[1]
             D = self.inner // self.heads
-            mask = attention_mask.to(q.dtype)
-            if mask.dim() == 3:
-                mask = mask[:, None]
-            o = F.scaled_dot_product_attention(*(t.reshape(B_, t.shape[1], self.heads, D).transpose(1, 2)
-                                                 for t in (q, k, v)), attn_mask=mask, scale=self.scale)
-            o = o.transpose(1, 2).reshape(B_, Nq, self.inner)
+            mask = attention_mask[:, None] if attention_mask.dim() == 3 else attention_mask
+            q4, k4, v4 = (t.reshape(B_, t.shape[1], self.heads, D) for t in (q, k, v))
+            o = FS.attend(q4, k4, v4, mask=mask, scale=self.scale) if q.is_cuda else None
+            if o is None:
+                mask = mask if mask.dtype == torch.bool else mask.to(q.dtype)
+                o = F.scaled_dot_product_attention(q4.transpose(1, 2), k4.transpose(1, 2), v4.transpose(1, 2),
+                                                   attn_mask=mask, scale=self.scale).transpose(1, 2)
+            o = o.reshape(B_, Nq, self.inner)
         else:
             o = attention_core(q.contiguous() if q.stride(-1) != 1 else q, k, v, self.heads, self.scale)
         o = F.linear(o, self.out_w, self.out_b)

@@ -11,7 +11,9 @@ that keeps the HF call contract (hidden_states, attention_mask, ...) -> hidden_s
 
 `DSEncoderLayer` (post-LN, the BERT family's layout):
   qkv    = x . Wqkv^T + b                 one GEMM over the concatenated q|k|v weights (bias in the GEMM epilogue)
-  ctx    = SDPA(q, k, v, mask)            non-causal, padding mask as an additive / boolean bias
+  ctx    = attention(q, k, v, mask)       the small-head flash kernel (head dim 32 / 64) reading q/k/v as strided
+                                          views of the fused projection, the padding mask as its per-key bias
+                                          (other head dims: the library attention)
   x1     = LN(ctx . Wo^T + bo + x)        GEMM (+bias epilogue), then the fused residual-add + LayerNorm kernel
   h      = gelu(x1 . W1^T + b1)           GEMM, then the fused bias + GELU kernel
   out    = LN(h . W2^T + b2 + x1)         GEMM (+bias epilogue), fused residual-add + LayerNorm
@@ -25,6 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import comm as dist
+from ..ops import flash_small as FS
 from ..ops.transformer import functional as DF
 
 _BERT_LIKE = ("BertLayer", "RobertaLayer", "XLMRobertaLayer", "ElectraLayer", "CamembertLayer", "RobertaPreLayerNormLayer")
@@ -107,11 +110,18 @@ class DSEncoderLayer(nn.Module):
     def _attn(self, x, attention_mask, is_causal):
         B, S, _ = x.shape
         qkv = F.linear(x, self.qkv_w, self.qkv_b).view(B, S, 3, self.nh, self.hd)
-        q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
-        mask = self._mask(attention_mask, q.dtype)
-        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, is_causal=bool(is_causal and mask is None))
-        ctx = ctx.transpose(1, 2).reshape(B, S, self.nh * self.hd)
-        return self._row_parallel(ctx, self.o_w, self.o_b)
+        causal = bool(is_causal and attention_mask is None)
+        ctx = None
+        if x.is_cuda and not torch.is_grad_enabled():
+            raw = attention_mask  # as given: an expanded (stride-0) padding mask is recognised by its strides
+            if raw is not None and raw.dim() == 2:
+                raw = raw[:, None, None, :].bool()
+            ctx = FS.attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], mask=raw, causal=causal)
+        if ctx is None:
+            mask = self._mask(attention_mask, qkv.dtype)
+            q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
+            ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, is_causal=causal).transpose(1, 2)
+        return self._row_parallel(ctx.reshape(B, S, self.nh * self.hd), self.o_w, self.o_b)
 
     def _mlp(self, x):
         if self.act is not None:

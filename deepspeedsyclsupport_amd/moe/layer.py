@@ -47,8 +47,14 @@ class MoE(torch.nn.Module):
         if not dist.is_initialized():
             return
         if self.expert_group_name not in groups._get_expert_parallel_group_dict():
-            groups._create_expert_and_data_parallel(self.ep_size,
-                                                    use_data_before_expert_parallel_=use_data_before_expert_parallel_)
+            if groups.mpu is None or not self.enable_expert_tensor_parallelism:
+                # no tensor parallelism, or experts deliberately kept whole: expert groups span the world and the
+                # MoE layer drops the tokens duplicated over tensor-parallel ranks (`moe/mappings.py`)
+                groups._create_expert_and_data_parallel(
+                    self.ep_size, use_data_before_expert_parallel_=use_data_before_expert_parallel_)
+            else:
+                groups._create_expert_data_and_model_parallel(
+                    self.ep_size, mpu=groups.mpu, use_data_before_expert_parallel_=use_data_before_expert_parallel_)
         self.deepspeed_moe._set_ep_group(groups._get_expert_parallel_group(self.expert_group_name))
 
     def forward(self, hidden_states, used_token=None):

@@ -14,7 +14,10 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from .. import comm as dist
+from ..parallel import groups
 from ..utils.logging import logger
+from . import mappings
+from .mappings import tensor_parallel_world_size
 
 uniform_map = {}
 gumbel_map = {}
@@ -92,6 +95,10 @@ def _route(logits, k, capacity_factor, min_capacity, noisy_gate_policy, drop_tok
         if dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         capacity = max(int(t), 1)
+    if groups._get_expert_model_parallel_world_size() == 1:
+        # the layer keeps 1/TP of the capacity slots per tensor-parallel rank (`mappings.drop_tokens`)
+        tp = tensor_parallel_world_size()
+        capacity = -(-capacity // tp) * tp
     # token priority inside an expert: random (RTS) or arrival order
     if use_rts and drop_tokens and training:
         prio = torch.rand(S, device=logits.device)
@@ -206,14 +213,26 @@ class MOELayer(torch.nn.Module):
         kept_idx = kept.nonzero(as_tuple=True)[0]
         dispatched = tokens.new_zeros(E * C, d_model)
         dispatched = dispatched.index_copy(0, flat_dst[kept_idx], tokens.index_select(0, src_tok[kept_idx]))
+        dispatched = dispatched.view(E, C, d_model)
+        full_C = C
+        drop = groups._get_expert_model_parallel_world_size() == 1 and tensor_parallel_world_size() > 1
+        if drop:
+            # tensor-parallel ranks hold the same tokens and the experts are not tensor parallel: each rank sends
+            # only its share of the capacity slots (reference `sharded_moe.py:505-512`)
+            dispatched = mappings.drop_tokens(dispatched, dim=1)
+            C = dispatched.shape[1]
         # [E, C, M] grouped by destination rank: experts e = r*L + l live on EP rank r
-        dispatched = _AllToAll.apply(self.ep_group, dispatched.view(E, C, d_model))
+        dispatched = _AllToAll.apply(self.ep_group, dispatched)
         # now [ep, L, C, M] of tokens from every rank for my L local experts -> [L, ep*C, M]
         L = self.num_local_experts
         local_in = dispatched.view(self.ep_size, L, C, d_model).transpose(0, 1).reshape(L * self.ep_size * C, d_model)
         expert_out = self._run_experts(local_in, L, C, d_model)
         back = expert_out.view(L, self.ep_size, C, d_model).transpose(0, 1).contiguous().view(E, C, d_model)
-        back = _AllToAll.apply(self.ep_group, back).view(E * C, d_model)
+        back = _AllToAll.apply(self.ep_group, back)
+        if drop:
+            back = mappings.gather_tokens(back, dim=1)  # every tensor-parallel rank needs all tokens again
+            C = full_C
+        back = back.reshape(E * C, d_model)
         gathered = back.index_select(0, flat_dst[kept_idx]) * w.reshape(-1)[kept_idx].unsqueeze(1).to(back.dtype)
         out = tokens.new_zeros(S, d_model).index_add(0, src_tok[kept_idx], gathered)
         self.l_aux = l_aux

@@ -74,6 +74,66 @@ def flash_small(q, k, v, bias1=None, bias2=None, b2_div=1, scale=None, dropout_p
     return FlashSmallFunc.apply(q, k, v, bias1, bias2, b2_div, scale, dropout_p, seed or 0)
 
 
+_CAUSAL_BIAS = {}
+BIAS2_MAX_BYTES = 64 << 20  # a per-(query, key) mask is expanded over heads for the kernel: only while that stays small
+
+
+def _causal_bias(H, S, dtype, device):
+    key = (H, S, dtype, str(device))
+    if key not in _CAUSAL_BIAS:
+        m = torch.full((S, S), torch.finfo(dtype).min, dtype=dtype, device=device).triu_(1)
+        _CAUSAL_BIAS[key] = m.expand(1, H, S, S).contiguous()
+    return _CAUSAL_BIAS[key]
+
+
+def attend(q, k, v, mask=None, scale=None, causal=False):
+    """Inference attention for encoder / diffusion blocks on the small-head kernel: q [B, Nq, H, D], k/v [B, Nk, H, D]
+    (views are fine) -> [B, Nq, H, D], or None when the kernel does not serve the case (the caller keeps its
+    library path). `mask` is what HF / diffusers modules hand around: boolean (True = attend) or additive, shaped
+    [B, Nk], [B, 1|Nq, Nk] or [B|1, 1|H, 1|Nq, Nk]. A mask that is constant over queries and heads (padding masks,
+    also when it arrives expanded with stride 0) travels as the per-key bias; anything else as the per-(query, key)
+    bias, shared over the batch when its batch dim is 1. `causal` adds the triangular bias (CLIP text tower)."""
+    B, Nq, H, D = q.shape
+    Nk = k.shape[1]
+    if not supported(q) or k.dtype != q.dtype or v.dtype != q.dtype or torch.is_grad_enabled() and Nq != Nk:
+        return None
+    b1 = b2 = None
+    b2_div = 1
+    if mask is not None:
+        m = mask
+        if m.dim() == 2:
+            m = m[:, None, None, :]
+        elif m.dim() == 3:
+            m = m[:, None]
+        if m.dim() != 4 or m.shape[-1] != Nk or m.shape[0] not in (1, B) or m.shape[1] not in (1, H) \
+                or m.shape[2] not in (1, Nq):
+            return None
+        # (read the strides before any conversion: a dtype cast of an expanded mask would densify it)
+        per_key = (m.shape[1] == 1 or m.stride(1) == 0) and (m.shape[2] == 1 or m.stride(2) == 0)
+        if per_key:
+            m = m[:, :1, :1, :]
+        elif m.shape[0] * H * Nq * Nk * q.element_size() > BIAS2_MAX_BYTES:
+            return None
+        if m.dtype == torch.bool:
+            m = torch.zeros(m.shape, dtype=q.dtype, device=q.device).masked_fill_(~m, torch.finfo(q.dtype).min)
+        else:
+            m = m.to(q.dtype)
+        if per_key:
+            b1 = m[:, 0, 0, :].expand(B, Nk).contiguous()
+        else:
+            b2 = m.expand(m.shape[0], H, Nq, Nk).contiguous()
+            b2_div = B // m.shape[0]
+    if causal:
+        if Nq != Nk:
+            return None
+        cb = _causal_bias(H, Nq, q.dtype, q.device)
+        if b2 is None:
+            b2, b2_div = cb, B
+        else:
+            b2 = b2 + cb  # (min + min saturates to -inf in bf16/fp16: still a masked key)
+    return flash_small(q, k, v, bias1=b1, bias2=b2, b2_div=b2_div, scale=scale)
+
+
 # ---------------------------------------------------------------------------------------------- host references
 _M0, _M1, _W0, _W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
 

@@ -39,6 +39,8 @@ def reset():
     _SEQUENCE_PARALLEL_GROUP = _SEQUENCE_DATA_PARALLEL_GROUP = None
     _SP_SIZE = 1
     mpu = None
+    global expert_tensor_parallel_world_size
+    expert_tensor_parallel_world_size = 1
 
 
 # ------------------------------------------------------------------------------------------- model parallel
@@ -163,6 +165,59 @@ def _create_expert_and_data_parallel(expert_parallel_size_, use_data_before_expe
                 g = dist.new_group(ranks)
                 if rank in ranks:
                     _EXPERT_PARALLEL_GROUP[name] = g
+
+
+def _get_expert_parallel_ranks(world_size, model_parallel_size_, expert_parallel_size_,
+                               use_data_before_expert_parallel_=False):
+    """Rank lists of the expert-parallel and expert-data-parallel groups under tensor (model) parallelism (reference
+    `groups.py:179-236`). Model-parallel groups are blocks of consecutive ranks; the ranks with the same position in
+    their block form one data-parallel line, and every line is cut into expert-parallel groups of
+    `expert_parallel_size_` members (E+D), or strided so that data-parallel neighbours stay adjacent (D+E). E.g.
+    world 16, model 2, expert 4: EP [0,2,4,6] [8,10,12,14] [1,3,5,7] [9,11,13,15]; EDP [0,8] [2,10] ... [7,15]."""
+    _ensure_divisibility(world_size, model_parallel_size_)
+    dp_world = world_size // model_parallel_size_
+    _ensure_divisibility(dp_world, expert_parallel_size_)
+    lines = []
+    for i in range(model_parallel_size_):
+        if use_data_before_expert_parallel_:
+            stride = dp_world // expert_parallel_size_
+            line = []
+            for d in range(stride):
+                line += list(range(i + d * model_parallel_size_, world_size, stride * model_parallel_size_))
+            lines.append(line)
+        else:
+            lines.append(list(range(i, world_size, model_parallel_size_)))
+    ep_groups, edp_groups = [], []
+    for line in lines:
+        parts = [line[i:i + expert_parallel_size_] for i in range(0, dp_world, expert_parallel_size_)]
+        ep_groups += parts
+        edp_groups += [list(t) for t in zip(*parts)]
+    return ep_groups, edp_groups
+
+
+def _create_expert_data_and_model_parallel(expert_parallel_size_, mpu, use_data_before_expert_parallel_=False):
+    """Expert groups for experts that ARE tensor parallel (reference `groups.py:239-290`): built inside each
+    data-parallel line of the mpu, and the expert tensor-parallel degree is recorded so the MoE layer keeps the
+    duplicated tokens (every TP rank of an expert needs them)."""
+    global expert_tensor_parallel_world_size
+    mp = mpu.get_model_parallel_world_size()
+    expert_tensor_parallel_world_size = mp
+    world_size, rank = dist.get_world_size(), dist.get_rank()
+    name = f"ep_size_{expert_parallel_size_}"
+    log_dist(f"Creating expert groups with model parallel size {mp}, expert parallel size {expert_parallel_size_}, "
+             f"world size {world_size}", ranks=[0])
+    if name in _EXPERT_DATA_PARALLEL_GROUP or name in _EXPERT_PARALLEL_GROUP:
+        return
+    ep_groups, edp_groups = _get_expert_parallel_ranks(world_size, mp, expert_parallel_size_,
+                                                       use_data_before_expert_parallel_)
+    for ranks in ep_groups:
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            _EXPERT_PARALLEL_GROUP[name] = g
+    for ranks in edp_groups:
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            _EXPERT_DATA_PARALLEL_GROUP[name] = g
 
 
 def _get_max_expert_size():

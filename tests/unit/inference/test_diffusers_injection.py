@@ -220,3 +220,49 @@ def test_generic_injection_gpu_kernels_and_graphs():
     assert calls, "self / cross attention did not run on the flash_small kernel"
     assert any(s[1] == 256 for s in calls)  # 16x16 tokens (captured once; replays do not re-enter Python)
     assert len(pipe.unet._graphed.graphs) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["key_bool", "key_additive_3d", "per_query_shared", "per_query_batch"])
+def test_masked_attention_runs_on_the_kernel(kind):
+    """An attention mask no longer sends the injected Attention to the library path: padding masks travel as the
+    kernel's per-key bias, per-(query, key) masks as its pair bias. Checked against the module's own fp32 math."""
+    from deepspeedsyclsupport_amd.module_inject import diffusers as DI
+    from deepspeedsyclsupport_amd.ops import flash_small as FS
+    torch.manual_seed(0)
+    B, Nq, Nk, heads, dh = 2, 96, 77, 4, 64
+    attn = Attention(128, cross_attention_dim=96, heads=heads, dim_head=dh, bias=True).cuda()
+    ds = DI.DSDiffusersAttention(copy.deepcopy(attn)).to(torch.bfloat16)
+    x = torch.randn(B, Nq, 128, device="cuda")
+    ctx = torch.randn(B, Nk, 96, device="cuda")
+    g = torch.Generator().manual_seed(2)
+    if kind == "key_bool":
+        mask = torch.ones(B, 1, 1, Nk, dtype=torch.bool)
+        mask[0, ..., 50:] = False
+        mask[1, ..., 9:] = False
+    elif kind == "key_additive_3d":
+        mask = torch.zeros(B, 1, Nk)
+        mask[0, :, 60:] = -1e4
+        mask = mask.expand(B, Nq, Nk)  # expanded over queries with stride 0, as diffusers' prepare_attention_mask does
+    elif kind == "per_query_shared":
+        mask = torch.randn(1, 1, Nq, Nk, generator=g)
+    else:
+        mask = torch.randn(B, heads, Nq, Nk, generator=g)
+    mask = mask.cuda()
+    ref_mask = mask if mask.dim() == 4 else mask[:, None]
+    calls = []
+    orig = FS.FlashSmallFunc.apply
+
+    def spy(*a):
+        calls.append((a[3] is not None, a[4] is not None))
+        return orig(*a)
+
+    FS.FlashSmallFunc.apply = spy
+    try:
+        with torch.no_grad():
+            got = ds(x.bfloat16(), encoder_hidden_states=ctx.bfloat16(), attention_mask=mask).float()
+            want = attn(x, encoder_hidden_states=ctx, attention_mask=ref_mask)
+    finally:
+        FS.FlashSmallFunc.apply = orig
+    assert calls == [(kind.startswith("key"), not kind.startswith("key"))]
+    assert ((got - want).abs().max() / want.abs().max()).item() < 3e-2

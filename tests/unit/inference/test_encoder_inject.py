@@ -126,7 +126,23 @@ def test_encoder_inject_bf16_gpu(kind):
     with torch.no_grad():
         ref = _out(m(input_ids=ids, attention_mask=mask)).float()
     eng = ds.init_inference(copy.deepcopy(m), dtype=torch.bfloat16, replace_with_kernel_inject=True)
-    with torch.no_grad():
-        out = _out(eng(input_ids=ids.cuda(), attention_mask=mask.cuda())).float().cpu()
+    from deepspeedsyclsupport_amd.ops import flash_small as FS
+    calls = []
+    orig = FS.FlashSmallFunc.apply
+
+    def spy(*a):
+        calls.append((a[3] is not None, a[4] is not None))
+        return orig(*a)
+
+    FS.FlashSmallFunc.apply = spy
+    try:
+        with torch.no_grad():
+            out = _out(eng(input_ids=ids.cuda(), attention_mask=mask.cuda())).float().cpu()
+    finally:
+        FS.FlashSmallFunc.apply = orig
     valid = mask.bool()
     assert (out[valid] - ref[valid]).abs().max().item() < 0.05 * ref.abs().max().item() + 0.05
+    # head dim 64: both layers' attention ran on the in-tree kernel with the padding mask as a bias, not on SDPA
+    assert len(calls) == 2 and all(b1 or b2 for b1, b2 in calls), calls
+    if kind != "clip_text":
+        assert all(b1 and not b2 for b1, b2 in calls), calls  # a pure padding mask is the per-key bias
