@@ -85,6 +85,13 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
         pipe = False
     cfg = config if isinstance(config, DeepSpeedConfig) else \
         DeepSpeedConfig(config, model.mpu() if pipe else mpu)
+    wq = cfg.param_dict.get("weight_quantization") or {}
+    if wq.get("quantized_initialization"):
+        # reference `runtime/zero/partition_parameters.py:317`: every linear / embedding weight is held as group-wise
+        # int4 / int8 codes; here the pass runs over the built model before the engine takes it
+        from .inference.quantization import _init_group_wise_weight_quantization
+        _init_group_wise_weight_quantization(
+            model, {"weight_quantization": {"quantized_initialization": wq["quantized_initialization"]}})
     if pipe:
         from .runtime.pipe.engine import PipelineEngine
         engine = PipelineEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
