@@ -163,9 +163,40 @@ class FlatLayoutSource(ShardSource):
                 for (name, shape, off, numel) in g["params"]:
                     key = gnames.get(name, name)
                     self.index.setdefault(key, []).append((si, g, (tuple(shape), off, numel)))
+        # frozen parameters: name -> [(state idx, frozen group index, group entry, (shape, offset, numel))]
+        self.frozen_index = OrderedDict()
+        for si, st in enumerate(self.states):
+            for gi, g in enumerate(st.get("frozen_layout") or []):
+                for (name, shape, off, numel) in g["params"]:
+                    self.frozen_index.setdefault(name, []).append((si, gi, g, (tuple(shape), off, numel)))
 
     def names(self):
         return list(self.index.keys())
+
+    def frozen_names(self):
+        return list(self.frozen_index.keys())
+
+    def get_frozen(self, name):
+        """Full value (saved dtype) of a frozen parameter cut out of the ranks' frozen shards, or None."""
+        ent = self.frozen_index.get(name)
+        if ent is None:
+            return None
+        shape, _, numel = ent[0][3]
+        out, covered = None, torch.zeros(numel, dtype=torch.bool)
+        for (si, gi, g, (_, off, _)) in ent:
+            shard = self.states[si]["frozen_shards"][gi]
+            lo = g["seg_lo"]
+            a, b = max(lo, off), min(lo + g["seg"], off + numel)
+            if a >= b:
+                continue
+            if out is None:
+                out = torch.zeros(numel, dtype=shard.dtype)
+            out[a - off:b - off] = shard[a - lo:b - lo]
+            covered[a - off:b - off] = True
+        if out is None or not bool(covered.all()):
+            raise ValueError(f"checkpoint shards cover only {int(covered.sum())}/{numel} elements of frozen "
+                             f"parameter '{name}' ({len(self.files)} files read)")
+        return out.view(shape)
 
     def _fetch(self, st, key, og, on_host):
         if key == "fp32":
@@ -424,7 +455,33 @@ def restore_from_source(optimizer, module, source, load_optimizer_states=True, s
     if step is not None:
         optimizer.set_step(step)
     optimizer._post_step_gather()
+    restore_frozen(optimizer, module, source)
     return step
+
+
+@torch.no_grad()
+def restore_frozen(optimizer, module, source):
+    """Frozen (partitioned, optimizer-less) parameters saved under another partitioning: each one is cut out of the
+    saving ranks' frozen shards and its local slice written into this rank's shard. Parameters the checkpoint does
+    not hold (saved with exclude_frozen_parameters) keep their current values."""
+    get = getattr(source, "get_frozen", None)
+    if get is None:
+        return 0
+    owned = {id(p) for p in optimizer.opt_params}
+    grouped = getattr(optimizer, "param_group", {})
+    n = 0
+    for name, p in module.named_parameters():
+        if id(p) in owned:
+            continue
+        v = get(name)
+        if v is None:
+            continue
+        if id(p) in grouped:
+            optimizer._scatter_param(p, v, "fp32", also_shard=True)
+        else:  # kept whole by this engine (one data-parallel rank, or below the persistence threshold)
+            p.data.copy_(v.reshape(p.shape))
+        n += 1
+    return n
 
 
 def layouts_match(saved, current):

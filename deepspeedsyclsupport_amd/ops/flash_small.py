@@ -11,6 +11,8 @@ Tensors are [Z, S, H, D] views (any z/s/h strides, unit last stride): Z folds th
 bias2 [Z / b2_div, H, S, S]. No [Z, H, S, S] tensor is ever materialised — not the bias sum, not P, not the dropout
 mask (regenerated in the backward from a Philox-4x32-7 stream keyed by (seed, z, h, query, key)).
 """
+import weakref
+
 import numpy as np
 import torch
 
@@ -86,13 +88,36 @@ def _causal_bias(H, S, dtype, device):
     return _CAUSAL_BIAS[key]
 
 
+_PER_KEY = {}  # id(mask) -> (weakref to it, its version counter, verdict)
+
+
+def _is_per_key(m):
+    """Is the 4-D mask constant over heads and queries? Broadcast dims and stride-0 (expanded) dims say so for free;
+    a dense [B, 1|H, Nq, Nk] mask (what HF's SDPA mask helpers build from a padding mask) is compared with its first
+    row once per tensor object: the verdict is remembered while that object lives, so the layers of an encoder that
+    all receive the same mask share one check. Inside a stream capture no host decision may depend on device data:
+    the mask then travels as the pair bias, which is always valid."""
+    if (m.shape[1] == 1 or m.stride(1) == 0) and (m.shape[2] == 1 or m.stride(2) == 0):
+        return True
+    if m.is_cuda and torch.cuda.is_current_stream_capturing():
+        return False
+    hit = _PER_KEY.get(id(m))
+    if hit is not None and hit[0]() is m and hit[1] == m._version:
+        return hit[2]
+    verdict = bool(torch.equal(m, m[:, :1, :1, :].expand_as(m)))
+    if len(_PER_KEY) > 256:
+        _PER_KEY.clear()
+    _PER_KEY[id(m)] = (weakref.ref(m), m._version, verdict)
+    return verdict
+
+
 def attend(q, k, v, mask=None, scale=None, causal=False):
     """Inference attention for encoder / diffusion blocks on the small-head kernel: q [B, Nq, H, D], k/v [B, Nk, H, D]
     (views are fine) -> [B, Nq, H, D], or None when the kernel does not serve the case (the caller keeps its
     library path). `mask` is what HF / diffusers modules hand around: boolean (True = attend) or additive, shaped
     [B, Nk], [B, 1|Nq, Nk] or [B|1, 1|H, 1|Nq, Nk]. A mask that is constant over queries and heads (padding masks,
-    also when it arrives expanded with stride 0) travels as the per-key bias; anything else as the per-(query, key)
-    bias, shared over the batch when its batch dim is 1. `causal` adds the triangular bias (CLIP text tower)."""
+    also when they arrive expanded) travels as the per-key bias; anything else as the per-(query, key) bias, shared
+    over the batch when its batch dim is 1. `causal` adds the triangular bias (CLIP text tower)."""
     B, Nq, H, D = q.shape
     Nk = k.shape[1]
     if not supported(q) or k.dtype != q.dtype or v.dtype != q.dtype or torch.is_grad_enabled() and Nq != Nk:
@@ -108,8 +133,7 @@ def attend(q, k, v, mask=None, scale=None, causal=False):
         if m.dim() != 4 or m.shape[-1] != Nk or m.shape[0] not in (1, B) or m.shape[1] not in (1, H) \
                 or m.shape[2] not in (1, Nq):
             return None
-        # (read the strides before any conversion: a dtype cast of an expanded mask would densify it)
-        per_key = (m.shape[1] == 1 or m.stride(1) == 0) and (m.shape[2] == 1 or m.stride(2) == 0)
+        per_key = _is_per_key(m)
         if per_key:
             m = m[:, :1, :1, :]
         elif m.shape[0] * H * Nq * Nk * q.element_size() > BIAS2_MAX_BYTES:

@@ -742,7 +742,7 @@ class DeepSpeedEngine(nn.Module):
     def _zero3_partitioned(self):
         opt = self.optimizer
         return self.zero_optimization_partition_weights() and opt is not None and \
-            any((not g.persistent) or g.partition for g in getattr(opt, "groups", []))
+            any((not g.persistent) or g.partition for g in getattr(opt, "all_groups", getattr(opt, "groups", [])))
 
     @torch.no_grad()
     def consolidated_16bit_state_dict(self, exclude_frozen_parameters=False, rank0_only=True):
@@ -759,7 +759,7 @@ class DeepSpeedEngine(nn.Module):
         keep = (not rank0_only) or dist.get_rank() == 0
         names = {id(p): n for n, p in self.module.named_parameters()}
         out = OrderedDict()
-        for g in opt.groups:
+        for g in opt.all_groups:
             if g.persistent and g.full is not None:
                 full = g.full
             else:
@@ -920,7 +920,7 @@ class DeepSpeedEngine(nn.Module):
         if self.save_non_zero_checkpoint:
             self.checkpoint_engine.save(state, self._get_ckpt_name(save_dir, tag))
         if zero:
-            osd = self.optimizer.state_dict()
+            osd = self.optimizer.state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
             zsd = dict(optimizer_state_dict=osd, ds_config=self._config.param_dict, ds_version=_version())
             self.checkpoint_engine.save(zsd, self._get_zero_ckpt_name(save_dir, tag))
             if self._ckpt_lead_rank == 0:
@@ -1047,6 +1047,9 @@ class DeepSpeedEngine(nn.Module):
                     continue
                 want = getattr(p, "ds_numel", p.numel())
                 if v.numel() == want and v.numel() > 0:
+                    if id(p) not in self.optimizer.param_group:  # kept whole on every rank (small / other dtype)
+                        p.data.copy_(v.reshape(p.shape))
+                        continue
                     # local copy into this rank's partition; the full buffers are refreshed once below
                     self.optimizer._scatter_param(p, v, "fp32", also_shard=True)
                     wrote = True

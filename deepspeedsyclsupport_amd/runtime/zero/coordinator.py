@@ -57,14 +57,22 @@ class ParamCoordinator:
                 groups._create_zero_param_parallel_group(zc.zero_hpz_partition_size)
             self.hpz = HpzState(groups._get_zero_param_intra_parallel_group())
         install_zero3_linear(opt.module)
-        for g in opt.groups:
+        self._deferred = []  # frozen groups whose release waits for the end of backward
+        for g in opt.all_groups:
             if g.persistent or g.module is None:
                 continue
             m = g.module
-            m._ds_fetch_group = g
-            self._hooks.append(m.register_forward_pre_hook(self._pre_fwd))
-            self._hooks.append(m.register_forward_hook(self._post_fwd))
-            self._hooks.append(m.register_full_backward_pre_hook(self._pre_bwd))
+            first = "_ds_fetch_groups" not in m.__dict__
+            m.__dict__.setdefault("_ds_fetch_groups", []).append(g)  # (trained and frozen params of one module)
+            if first:
+                self._hooks.append(m.register_forward_pre_hook(self._pre_fwd))
+                self._hooks.append(m.register_forward_hook(self._post_fwd))
+                self._hooks.append(m.register_full_backward_pre_hook(self._pre_bwd))
+            if g.frozen and not m.__dict__.get("_ds_frozen_hooked"):
+                # trained groups are released when their last gradient arrives; frozen ones produce none, so the
+                # module's backward hook (input gradients computed) releases them
+                m.__dict__["_ds_frozen_hooked"] = True
+                self._hooks.append(m.register_full_backward_hook(self._post_bwd))
         for m in opt.module.modules():
             if m.__dict__.get("_ds_external_params"):
                 self.install_external(m)
@@ -110,16 +118,17 @@ class ParamCoordinator:
 
     # ----------------------------------------------------------------------------------- hooks
     def _pre_fwd(self, m, inputs):
-        self.fetch(m._ds_fetch_group)
+        for g in m._ds_fetch_groups:
+            self.fetch(g)
 
     def _post_fwd(self, m, inputs, outputs):
         if self.in_backward or torch._C._current_graph_task_id() != -1:
             return  # activation-checkpoint recompute inside backward: keep params for the module's backward
-        g = m._ds_fetch_group
-        if self._keep_for_reuse(g):
-            self.profiler.count("reuse_hit", g.numel)
-            return
-        self.release(g)
+        for g in m._ds_fetch_groups:
+            if self._keep_for_reuse(g):
+                self.profiler.count("reuse_hit", g.numel)
+                continue
+            self.release(g)
 
     def _keep_for_reuse(self, g):
         """Keep a just-used group gathered when the trace says it is fetched again soon enough."""
@@ -132,7 +141,18 @@ class ParamCoordinator:
         return d is not None and d <= self.max_reuse and self.live_numel <= self.max_live
 
     def _pre_bwd(self, m, grad_output):
-        self.fetch(m._ds_fetch_group)
+        for g in m._ds_fetch_groups:
+            self.fetch(g)
+
+    def _post_bwd(self, m, grad_input, grad_output):
+        frozen = [g for g in m._ds_fetch_groups if g.frozen]
+        if all(gi is None for gi in grad_input):
+            # no input needs a gradient: autograd fires this hook BEFORE the module's own backward work, so the
+            # weights stay until the pass is over
+            self._deferred.extend(frozen)
+            return
+        for g in frozen:
+            self.release_after_backward(g)
 
     # ----------------------------------------------------------------------------------- core
     def _gather(self, g):
@@ -240,7 +260,7 @@ class ParamCoordinator:
             return
         budget = self.prefetch_bucket_size
         i = self.pos
-        groups = self.opt.groups
+        groups = self.opt.all_groups
         while i < len(self.trace) and budget > 0:
             g = groups[self.trace[i]]
             if g.status == ZeroParamStatus.NOT_AVAILABLE:
@@ -252,7 +272,7 @@ class ParamCoordinator:
 
     def _reuse_distances(self):
         """For each trace position, the elements gathered between it and the next fetch of the same group."""
-        groups = self.opt.groups
+        groups = self.opt.all_groups
         prefix = [0]
         for gi in self.trace:
             prefix.append(prefix[-1] + groups[gi].numel)
@@ -269,6 +289,9 @@ class ParamCoordinator:
 
     def end_backward(self):
         self.in_backward = False
+        for g in self._deferred:
+            self.release_after_backward(g)
+        self._deferred = []
 
     def reset_step(self):
         """End of an optimizer step: close the trace, release anything still gathered."""
@@ -283,7 +306,7 @@ class ParamCoordinator:
             self.trace = []
             self.mode = RECORD
         self.pos = 0
-        for g in self.opt.groups:
+        for g in self.opt.all_groups:
             if not g.persistent and g.status != ZeroParamStatus.NOT_AVAILABLE:
                 self.release(g)
 

@@ -96,6 +96,8 @@ class FlatGroup:
         self.reduced_this_pass = False
         self.runs = []            # (seg_lo, seg_hi, opt_group_idx, master_off, on_host)
         self.trace_pos = []
+        self.frozen = False       # parameters the optimizer does not own: fetched / released, never reduced or stepped
+        self.pieces = []
 
     @property
     def seg_lo(self):
@@ -201,7 +203,7 @@ class FlatZeroOptimizer(ZeROOptimizer):
         self._install_grad_hooks()
         self.coordinator = None
         if self.stage == 3 and (self.dp > 1 or self.offload_param or self.force_partition):
-            from .coordinator import ParamCoordinator
+            from .coordinator import ParamCoordinator  # (also when only frozen groups are fetched)
             self.coordinator = ParamCoordinator(self, prefetch_bucket_size=self.zc.prefetch_bucket_size,
                                                 max_live_parameters=self.zc.max_live_parameters,
                                                 max_reuse_distance=self.zc.max_reuse_distance)
@@ -291,19 +293,60 @@ class FlatZeroOptimizer(ZeROOptimizer):
             g.expert = bool(self.optimizer.param_groups[og].get("moe", False))
             g.sparse = bool(d.get("sparse", False))
             self.groups.append(g)
+        self._build_frozen_groups()
         self.param_group = {}
         import weakref
         ref = weakref.ref(self)
-        for g in self.groups:
+        for g in self.all_groups:
             for i, p in enumerate(g.params):
                 self.param_group[id(p)] = (g, i)
                 p._ds_zero_optimizer = ref  # lets utils.tensor_fragment.safe_get_* find the owner
         self._materialize_buffers()
 
+    @property
+    def all_groups(self):
+        """Optimizer-owned groups followed by the frozen ones; `FlatGroup.idx` indexes this list."""
+        return self.groups + self.frozen_groups
+
+    def _build_frozen_groups(self):
+        """ZeRO-3 partitions every module parameter, not only the trained ones (reference `stage3.py:419-470`,
+        `parameter_offload.py:240-260`): with adapters on a frozen base model the frozen weights are most of the
+        memory. Parameters the optimizer does not own (requires_grad=False, or simply not handed to it) get fetch
+        groups of their own, one per owning module: partitioned, gathered before the module's forward / backward and
+        released after, optionally homed on the host / NVMe with offload_param, but never reduced or stepped. Small
+        ones (below the persistence threshold) and those of another dtype stay whole on every rank."""
+        self.frozen_groups = []
+        if self.stage != 3:
+            return
+        fetched = self.dp > 1 or self.offload_param or self.force_partition
+        thr = self.zc.param_persistence_threshold if fetched else 0
+        seen = set(self.param_to_og)
+        base = len(self.groups)
+        for name, m in self.module.named_modules():
+            ps = [p for p in m.parameters(recurse=False) if id(p) not in seen]
+            if not ps:
+                continue
+            seen.update(id(p) for p in ps)
+            big = [p for p in ps if fetched and p.dtype == self.dtype and _pnumel(p) >= thr]
+            for p in ps:
+                if not any(p is q for q in big) and getattr(p, "ds_tensor", None) is not None \
+                        and p.data.numel() != p.ds_numel:
+                    # built partitioned under zero.Init but kept whole here
+                    from .partition_parameters import gather_partitioned_param
+                    p.data = gather_partitioned_param(p).clone()
+                    del p.ds_tensor
+            if not big:
+                continue
+            multi = self.dp > 1 or self.force_partition
+            g = FlatGroup(base + len(self.frozen_groups), big, self.dp, self.rank, multi, False, self.device,
+                          self.dtype, m, dp_group=self.dp_group)
+            g.frozen = True
+            self.frozen_groups.append(g)
+
     @torch.no_grad()
     def _materialize_buffers(self):
         """Move parameter data into flat buffers (full for persistent groups, shard-only for ZeRO-3)."""
-        for g in self.groups:
+        for g in self.all_groups:
             g._opt = self
             full = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
             for i, p in enumerate(g.params):
@@ -534,7 +577,7 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_ready_hook))
 
     def coordinator_needed(self):
-        return self.stage == 3 and any(not g.persistent for g in self.groups)
+        return self.stage == 3 and any(not g.persistent for g in self.all_groups)
 
     def _point_grads(self, g):
         for i, p in enumerate(g.params):
@@ -1043,10 +1086,23 @@ class FlatZeroOptimizer(ZeROOptimizer):
         if key == "fp32" and also_shard:
             g.shard[a:a + n].copy_(values)
 
+    def _frozen_full(self, g):
+        """Gathered flat buffer of a frozen group (its 16-bit weights are the only state it has)."""
+        shard = g.shard if g.shard.device == self.device else g.shard.to(self.device)
+        if not g.partition:
+            return shard
+        full = torch.empty(g.padded, dtype=shard.dtype, device=self.device)
+        dist.all_gather_into_tensor(full, shard.contiguous(), group=g.dp_group)
+        return full
+
     @torch.no_grad()
     def _gather_param(self, p, key):
         self.join_offload()
         g, i = self.param_group[id(p)]
+        if g.frozen:
+            if key != "fp32":
+                return None
+            return self._frozen_full(g)[g.offsets[i]:g.offsets[i] + g.numels[i]].view(p.ds_shape).float()
         seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
         for run in g.runs:
             src = self._run_read(g, run, key, run[0], run[1])
@@ -1065,6 +1121,12 @@ class FlatZeroOptimizer(ZeROOptimizer):
         g, i = self.param_group[id(p)]
         flat = value.reshape(-1).to(torch.float32)
         a = g.offsets[i]
+        if g.frozen:
+            if key == "fp32":
+                lo, hi = max(g.seg_lo, a), min(g.seg_lo + g.seg, a + g.numels[i])
+                if lo < hi:
+                    g.shard[lo - g.seg_lo:hi - g.seg_lo].copy_(flat[lo - a:hi - a])
+            return
         for run in g.runs:
             lo, hi = g.seg_lo + run[0], g.seg_lo + run[1]
             x0, x1 = max(lo, a), min(hi, a + g.numels[i])
@@ -1076,6 +1138,11 @@ class FlatZeroOptimizer(ZeROOptimizer):
         self.join_offload()
         g, i = self.param_group[id(p)]
         a, n = g.offsets[i], g.numels[i]
+        if g.frozen:
+            lo, hi = max(g.seg_lo, a), min(g.seg_lo + g.seg, a + n)
+            if key != "fp32" or lo >= hi:
+                return None
+            return g.shard[lo - g.seg_lo:hi - g.seg_lo].to(self.device, torch.float32)
         parts = []
         for run in g.runs:
             lo, hi = g.seg_lo + run[0], g.seg_lo + run[1]
@@ -1129,6 +1196,8 @@ class FlatZeroOptimizer(ZeROOptimizer):
     def get_full_grad(self, p):
         """Averaged fp32 gradient of one param (valid between backward at the boundary and step)."""
         g, i = self.param_group[id(p)]
+        if g.frozen:
+            return None
         seg32 = torch.zeros(g.seg, dtype=torch.float32, device=self.device)
         if g.mode == self.LOCAL:
             if p.grad is not None:
@@ -1200,7 +1269,7 @@ class FlatZeroOptimizer(ZeROOptimizer):
             out[p.moff:p.moff + p.n].copy_(self._run_read(p.group, run, "fp32", p.s, p.s + p.n))
         return out
 
-    def state_dict(self):
+    def state_dict(self, exclude_frozen_parameters=False):
         self.join_offload()
         sd = OrderedDict()
         sd[CK.ZERO_STAGE] = self.stage
@@ -1222,8 +1291,32 @@ class FlatZeroOptimizer(ZeROOptimizer):
                                                        self.off.read_state(og, "exp_avg_sq", 0, n).clone(),
                                                        self.off.step_count[og]]
         sd[CK.FLAT_LAYOUT] = self.layout()
+        if self.frozen_groups and not exclude_frozen_parameters:
+            sd["frozen_layout"] = self.frozen_layout()
+            sd["frozen_shards"] = [g.shard.detach().to("cpu").clone() for g in self.frozen_groups]
         sd[CK.DS_VERSION] = _version()
         return sd
+
+    def frozen_layout(self):
+        """Per frozen group: segment geometry and (name, shape, offset, numel) of its parameters, so any reader can
+        cut every parameter out of the ranks' shards (reference: `frozen_param_fragments`, `engine.py:3432-3460`)."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        return [dict(seg=g.seg, dp=g.dp, seg_lo=int(g.seg_lo), padded=int(g.padded), rank=int(g.rank),
+                     partition=bool(g.partition),
+                     params=[(names.get(id(p), f"param_{id(p)}"), list(p.ds_shape), g.offsets[i], g.numels[i])
+                             for i, p in enumerate(g.params)]) for g in self.frozen_groups]
+
+    @torch.no_grad()
+    def load_frozen_shards(self, sd):
+        """Positional restore of the frozen shards when the saved geometry is this rank's; returns False otherwise
+        (the caller then rebuilds them from every rank's file, `checkpoint/zero_checkpoint.restore_frozen`)."""
+        if not self.frozen_groups:
+            return True
+        if sd.get("frozen_layout") != self.frozen_layout():
+            return False
+        for g, t in zip(self.frozen_groups, sd["frozen_shards"]):
+            g.shard.copy_(t)
+        return True
 
     @torch.no_grad()
     def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
@@ -1266,6 +1359,8 @@ class FlatZeroOptimizer(ZeROOptimizer):
                     src = (host if on_host else dev)[og][moff:moff + e - s]
                     self._run_write(g, run, "fp32", s, src.to(self.device), also_shard=True)
             self._post_step_gather()
+        if "frozen_shards" in sd:
+            self.load_frozen_shards(sd)
 
     def refresh_from_module(self):
         """Re-read master weights from the (possibly externally modified) bf16 shards."""

@@ -129,6 +129,32 @@ def _reassemble(states, key):
     return out
 
 
+def _reassemble_frozen(states):
+    """Frozen parameters ZeRO-3 partitioned without optimizer state: name -> full fp32 tensor, cut out of every
+    rank's `frozen_shards` by its `frozen_layout` (segment geometry + per-parameter offsets)."""
+    index = OrderedDict()
+    for r, st in enumerate(states):
+        for gi, g in enumerate(st.get("frozen_layout") or []):
+            for (name, shape, off, numel) in g["params"]:
+                index.setdefault(name, []).append((r, gi, g, tuple(shape), off, numel))
+    out = OrderedDict()
+    for name, ents in index.items():
+        shape, numel = ents[0][3], ents[0][5]
+        buf = torch.zeros(numel, dtype=torch.float32)
+        cov = torch.zeros(numel, dtype=torch.bool)
+        for (r, gi, g, _, off, _) in ents:
+            shard = states[r]["frozen_shards"][gi]
+            lo = g["seg_lo"]
+            a, b = max(lo, off), min(lo + g["seg"], off + numel)
+            if a < b:
+                buf[a - off:b - off] = shard[a - lo:b - lo].float()
+                cov[a - off:b - off] = True
+        if not bool(cov.all()):
+            raise ValueError(f"frozen '{name}': the {len(states)} shard files cover {int(cov.sum())}/{numel} elements")
+        out[name] = buf.view(shape)
+    return out
+
+
 def load_optim_states(ds_checkpoint_dir):
     return [_load(f)[OPTIMIZER_STATE_DICT] for f in get_optim_files(ds_checkpoint_dir)]
 
@@ -136,6 +162,8 @@ def load_optim_states(ds_checkpoint_dir):
 def _get_fp32_state_dict_from_zero_checkpoint(ds_checkpoint_dir, exclude_frozen_parameters=False):
     states = load_optim_states(ds_checkpoint_dir)
     out = _reassemble(states, "fp32")
+    if not exclude_frozen_parameters:
+        out.update(_reassemble_frozen(states))
     # non-expert parameters whose 16-bit placeholders are empty (ZeRO-3) come only from the shards above
     # buffers (and any non-partitioned tensors) come from the 16-bit model file
     try:
