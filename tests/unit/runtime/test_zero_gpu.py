@@ -160,3 +160,54 @@ def test_split_adam_kernel_matches_fp32_master():
             torch.testing.assert_close(j, p, rtol=1e-5, atol=2e-8)
             torch.testing.assert_close(m2, m, rtol=1e-5, atol=1e-10)
             assert bool(((hi.float() - j).abs() <= j.abs() * 2.0**-8).all())
+
+
+@pytest.mark.parametrize("pdev", [None, "cpu"])
+def test_frozen_parameters_partitioned_on_one_gpu(pdev, monkeypatch):
+    """A frozen base (embedding, attention and norms of layer 0) with the rest trained, on the partitioned device
+    path: frozen weights are fetched on the all-gather stream, released by the module backward hook, optionally homed
+    in pinned host memory, and the trained ones follow plain PyTorch with the same parameters frozen."""
+    import deepspeedsyclsupport_amd as ds
+    from ..simple_model import base_config
+    monkeypatch.setenv("DS_ZERO_FORCE_PARTITION", "1")
+
+    def frozen_of(m):
+        return [p for n, p in m.named_parameters() if "embed_tokens" in n or "layers.0.self_attn" in n
+                or "layers.0.input_layernorm" in n]
+
+    torch.manual_seed(0)
+    ref_m = tiny_llama(hidden_size=128, intermediate_size=256, num_attention_heads=4).cuda()
+    for p in frozen_of(ref_m):
+        p.requires_grad_(False)
+    opt = torch.optim.AdamW([p for p in ref_m.parameters() if p.requires_grad], lr=3e-3, weight_decay=0.01)
+    ref = []
+    for x in _data(5, 5):
+        loss = ref_m(x, labels=x)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_([p for p in ref_m.parameters() if p.requires_grad], 1.0)
+        opt.step()
+        ref.append(float(loss))
+
+    torch.manual_seed(0)
+    m = tiny_llama(hidden_size=128, intermediate_size=256, num_attention_heads=4)
+    for p in frozen_of(m):
+        p.requires_grad_(False)
+    before = [p.detach().clone() for p in frozen_of(m)]
+    cfg = base_config(stage=3, lr=3e-3, mb=2, clip=1.0, dtype="fp32")
+    cfg["zero_optimization"]["stage3_param_persistence_threshold"] = 0
+    if pdev:
+        cfg["zero_optimization"]["offload_param"] = {"device": pdev, "pin_memory": True}
+    eng, *_ = ds.initialize(model=m, config=cfg, model_parameters=[p for p in m.parameters() if p.requires_grad])
+    assert eng.optimizer.frozen_groups and all(g.partition for g in eng.optimizer.frozen_groups)
+    got = []
+    for x in _data(5, 5):
+        loss = eng(x, labels=x)
+        eng.backward(loss)
+        eng.step()
+        got.append(float(loss))
+    assert got == pytest.approx(ref, rel=2e-3, abs=2e-3), (got, ref)
+    assert all(p.numel() == 0 for p in m.parameters())
+    with ds.zero.GatheredParameters(frozen_of(m)):
+        for p, b in zip(frozen_of(m), before):
+            assert torch.equal(p.detach().cpu(), b)
