@@ -61,6 +61,13 @@ class DeepSpeedDataSampler:
     def __len__(self):
         return self.total
 
+    def set_custom_curriculum_learning_schedule(self, schedule_func_dict):
+        """{metric name: fn(global step) -> difficulty} for metrics whose schedule_type is "custom" (reference
+        `data_sampling/data_sampler.py:97-100`)."""
+        for name, fn in schedule_func_dict.items():
+            if name in self.schedulers:
+                self.schedulers[name].set_custom_get_difficulty(fn)
+
     def _eligible(self):
         mask = np.ones(self.total, dtype=bool)
         for name, (vals, dtype) in self.metrics.items():

@@ -664,6 +664,7 @@ class DeepSpeedEngine(nn.Module):
 
     def step(self, lr_kwargs=None):
         self.timers(STEP_MICRO_TIMER).start()
+        self._step_applied = False
         if self.is_gradient_accumulation_boundary():
             self.gas_boundary_ctr += 1
             from .activation_checkpointing import checkpointing as _ckpt
@@ -674,6 +675,7 @@ class DeepSpeedEngine(nn.Module):
             if self.optimizer is not None:
                 self.optimizer.step()
                 overflow = self.optimizer.overflow
+                self._step_applied = not overflow
                 if overflow:
                     self.skipped_steps += 1
                 elif self.lr_scheduler is not None:
@@ -1075,6 +1077,190 @@ class DeepSpeedEngine(nn.Module):
             self.optimizer.refresh_from_module()
         return []
 
+
+    # ============================================================================================ small API surface
+    def destroy(self):
+        """Drop the hooks and buffers the engine hung on the module (reference `runtime/engine.py:369-373`)."""
+        opt = self.optimizer
+        if opt is not None:
+            opt.join_offload()
+            if getattr(opt, "coordinator", None) is not None:
+                opt.coordinator.remove_hooks()
+            for h in getattr(opt, "_hooks", []):
+                h.remove()
+            opt._hooks = []
+        if self.checkpoint_engine is not None:
+            self.checkpoint_engine.commit("destroy")
+
+    def was_step_applied(self) -> bool:
+        """False when the last `step()` fell inside an accumulation window or was skipped for overflow (reference
+        `runtime/engine.py:1300-1309`)."""
+        return bool(getattr(self, "_step_applied", False))
+
+    def get_batch_info(self):
+        """(train_batch_size, train_micro_batch_size_per_gpu, gradient_accumulation_steps)."""
+        return self.train_batch_size(), self.train_micro_batch_size_per_gpu(), self.gradient_accumulation_steps()
+
+    def set_train_micro_batch_size(self, micro_batch_size):
+        """New micro-batch size at the same accumulation depth (reference `runtime/engine.py:446-452`)."""
+        gas = self.gradient_accumulation_steps()
+        self._config.train_batch_size = micro_batch_size * gas * self.dp_world_size
+        self._config.train_micro_batch_size_per_gpu = micro_batch_size
+
+    def get_type(self):
+        """Optimizer hyper-parameter "type" per param group (reference `runtime/engine.py:1823`)."""
+        return [g.get("type") for g in self.optimizer.param_groups] if self.optimizer is not None else None
+
+    def get_data_types(self):
+        """(model dtype, gradient-accumulation dtype), reference `runtime/engine.py:1031-1044`."""
+        model_dtype = self._dtype()
+        acc = self._config.grad_accum_dtype
+        acc_dtype = {None: None, "fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}.get(acc)
+        if acc_dtype is None:
+            acc_dtype = torch.float32 if model_dtype == torch.bfloat16 else model_dtype
+        return model_dtype, acc_dtype
+
+    def dynamic_loss_scale(self):
+        return self._config.loss_scale == 0
+
+    def postscale_gradients(self):
+        return not self._config.prescale_gradients
+
+    def zero_cpu_offload(self):
+        return self.zero_offload_optimizer() is not None and \
+            str(getattr(self.zero_offload_optimizer().device, "value", self.zero_offload_optimizer().device)) == "cpu"
+
+    zero_use_cpu_optimizer = zero_cpu_offload
+
+    def zero_has_nvme_offload(self):
+        devs = [getattr(o, "device", None) for o in (self.zero_offload_optimizer(), self.zero_offload_param())
+                if o is not None]
+        return any(str(getattr(d, "value", d)) == "nvme" for d in devs)
+
+    def zero_partial_offload(self):
+        o = self.zero_offload_optimizer()
+        return float(getattr(o, "ratio", 1.0)) if o is not None else 1.0
+
+    def get_pld_theta(self):
+        return self.progressive_layer_drop.get_theta() if self.progressive_layer_drop is not None else None
+
+    def pld_theta(self):
+        return self._config.pld_params.get("theta", 1.0) if self._config.pld_params else None
+
+    def pld_gamma(self):
+        return self._config.pld_params.get("gamma", 0.001) if self._config.pld_params else None
+
+    def random_ltd_enabled(self):
+        de = self._config.data_efficiency_config or {}
+        return bool(de.get("enabled", False) and de.get("data_routing", {}).get("random_ltd", {}).get("enabled", False))
+
+    def random_ltd_config(self):
+        return (self._config.data_efficiency_config or {}).get("data_routing", {}).get("random_ltd", {})
+
+    def data_sampling_enabled(self):
+        de = self._config.data_efficiency_config or {}
+        return bool(de.get("enabled", False) and de.get("data_sampling", {}).get("enabled", False))
+
+    def data_sampling_config(self):
+        return (self._config.data_efficiency_config or {}).get("data_sampling", {})
+
+    def curriculum_learning_config(self):
+        return self.data_sampling_config().get("curriculum_learning", {})
+
+    def set_custom_curriculum_learning_schedule(self, schedule_func_dict):
+        """Install client difficulty schedules (reference `runtime/engine.py:1742-1744`): {metric: fn(step)}."""
+        dl = self.training_dataloader
+        sampler = getattr(dl, "data_sampler", None)
+        if sampler is None or not hasattr(sampler, "set_custom_curriculum_learning_schedule"):
+            raise RuntimeError("no curriculum data sampler: enable data_efficiency.data_sampling.curriculum_learning "
+                               "and build the loader with engine.deepspeed_io")
+        sampler.set_custom_curriculum_learning_schedule(schedule_func_dict)
+
+    def flops_profiler_enabled(self):
+        return self._config.flops_profiler_config.enabled
+
+    def flops_profiler_profile_step(self):
+        return self._config.flops_profiler_config.profile_step
+
+    def flops_profiler_module_depth(self):
+        return self._config.flops_profiler_config.module_depth
+
+    def flops_profiler_top_modules(self):
+        return self._config.flops_profiler_config.top_modules
+
+    def flops_profiler_detailed(self):
+        return self._config.flops_profiler_config.detailed
+
+    def flops_profiler_output_file(self):
+        return self._config.flops_profiler_config.output_file
+
+    def autotuning_enabled(self):
+        return bool((self._config.autotuning_config or {}).get("enabled", False))
+
+    def autotuning_metric(self):
+        return (self._config.autotuning_config or {}).get("metric", "throughput")
+
+    def autotuning_metric_path(self):
+        return (self._config.autotuning_config or {}).get("metric_path")
+
+    def autotuning_start_profile_step(self):
+        return (self._config.autotuning_config or {}).get("start_profile_step", 3)
+
+    def autotuning_end_profile_step(self):
+        return (self._config.autotuning_config or {}).get("end_profile_step", 5)
+
+    @staticmethod
+    def is_map_style_dataset(obj):
+        return hasattr(obj, "__getitem__") and hasattr(obj, "__len__")
+
+    @staticmethod
+    def is_iterable_style_dataset(obj):
+        return isinstance(obj, torch.utils.data.IterableDataset)
+
+    def empty_partition_cache(self):
+        """Release every gathered ZeRO-3 parameter now (reference `runtime/engine.py:3594-3602`), e.g. between an
+        evaluation pass and the next training step."""
+        coord = getattr(self.optimizer, "coordinator", None) if self.optimizer is not None else None
+        if coord is not None:
+            for g in self.optimizer.all_groups:
+                if not g.persistent:
+                    coord.release(g)
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def load_module_state_dict(self, checkpoint=None, strict=True, custom_load_fn=None, fetch_z3_params=False):
+        """Load module weights from a loaded checkpoint dict (its "module" entry) or a plain state dict (reference
+        `runtime/engine.py:2553-2590`); the optimizer's master weights follow the loaded values."""
+        sd = checkpoint.get("module", checkpoint) if isinstance(checkpoint, dict) else checkpoint
+        if custom_load_fn is not None:
+            custom_load_fn(src=sd, dst=self.module)
+            if self.optimizer is not None and not self._zero3_partitioned():
+                self.optimizer.refresh_from_module()
+            return []
+        return self._load_module_state(dict(sd or {}), strict=strict)
+
+    def update_optimizer_step(self, step):
+        """Overwrite the optimizer's step counter (reference `runtime/engine.py:2600-2614`)."""
+        if hasattr(self.optimizer, "set_step"):
+            self.optimizer.set_step(step)
+        else:
+            for st in self.optimizer.state.values():
+                if "step" in st:
+                    st["step"] = step
+
+    def print_forward_breakdown(self, fwd_time):
+        """MoE time split of the forward pass (reference `runtime/engine.py:1776-1796`)."""
+        gate = moe = falltoall = salltoall = 0.0
+        for _, m in self._moe_layers():
+            layer = m.deepspeed_moe
+            gate += getattr(layer.gate, "gate_time", 0.0)
+            moe += layer.time_moe
+            falltoall += layer.time_falltoall
+            salltoall += layer.time_salltoall
+        log_dist(f"time (ms) | fwd: {fwd_time:.2f} (fwd_moe: {moe:.2f}, 1st_a2a: {falltoall:.2f}, "
+                 f"2nd_a2a: {salltoall:.2f}, top_k: {gate:.2f})", ranks=[0])
+
+
     def save_16bit_model(self, save_dir, save_filename="pytorch_model.bin", exclude_frozen_parameters=False):
         """Consolidated 16-bit weights, streamed group by group to rank 0 (reference `runtime/engine.py:3477`)."""
         sd = self.consolidated_16bit_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
@@ -1086,6 +1272,70 @@ class DeepSpeedEngine(nn.Module):
 
     save_fp16_model = save_16bit_model
 
+
+
+# ------------------------------------------------------------------------------------------------ accessor surface
+# The reference engine exposes most configuration values as zero-argument methods (`runtime/engine.py:470-880`);
+# client code and integrations (HF Trainer, Megatron-DeepSpeed) call them. They are generated from two tables:
+# method name -> attribute of the parsed config, and method name -> field of the ZeRO sub-config.
+_CONFIG_ACCESSORS = {
+    "dump_state": "dump_state", "optimizer_name": "optimizer_name", "optimizer_params": "optimizer_params",
+    "optimizer_legacy_fusion": "optimizer_legacy_fusion", "scheduler_name": "scheduler_name",
+    "scheduler_params": "scheduler_params", "amp_params": "amp_params", "aio_config": "aio_config",
+    "dynamic_loss_scale_args": "dynamic_loss_scale_args", "initial_dynamic_scale": "initial_dynamic_scale",
+    "gradient_predivide_factor": "gradient_predivide_factor", "sparse_gradients_enabled": "sparse_gradients_enabled",
+    "communication_data_type": "communication_data_type", "dataloader_drop_last": "dataloader_drop_last",
+    "elasticity_enabled": "elasticity_enabled", "pld_enabled": "pld_enabled", "pld_params": "pld_params",
+    "curriculum_enabled_legacy": "curriculum_enabled_legacy", "curriculum_params_legacy": "curriculum_params_legacy",
+    "data_efficiency_enabled": "data_efficiency_enabled", "data_efficiency_config": "data_efficiency_config",
+    "eigenvalue_enabled": "eigenvalue_enabled", "eigenvalue_verbose": "eigenvalue_verbose",
+    "eigenvalue_max_iter": "eigenvalue_max_iter", "eigenvalue_tol": "eigenvalue_tol",
+    "eigenvalue_stability": "eigenvalue_stability", "eigenvalue_layer_name": "eigenvalue_layer_name",
+    "eigenvalue_layer_num": "eigenvalue_layer_num",
+    "eigenvalue_gas_boundary_resolution": "eigenvalue_gas_boundary_resolution",
+    "checkpoint_tag_validation_enabled": "checkpoint_tag_validation_enabled",
+    "checkpoint_tag_validation_fail": "checkpoint_tag_validation_fail",
+    "load_universal_checkpoint": "load_universal_checkpoint", "use_node_local_storage": "use_node_local_storage",
+    "graph_harvesting": "graph_harvesting", "fp16_auto_cast": "fp16_auto_cast",
+    "fp16_master_weights_and_gradients": "fp16_master_weights_and_gradients",
+    "zero_allow_untested_optimizer": "zero_allow_untested_optimizer",
+    "zero_force_ds_cpu_optimizer": "zero_force_ds_cpu_optimizer", "mics_shard_size": "mics_shard_size",
+    "swap_tensor_config": "aio_config",
+}
+_ZERO_ACCESSORS = {
+    "zero_reduce_scatter": "reduce_scatter", "zero_overlap_comm": "overlap_comm",
+    "zero_contiguous_gradients": "contiguous_gradients", "zero_reduce_bucket_size": "reduce_bucket_size",
+    "zero_multi_rank_bucket_allreduce": "use_multi_rank_bucket_allreduce",
+    "zero_allgather_bucket_size": "allgather_bucket_size", "zero_allgather_partitions": "allgather_partitions",
+    "zero_sub_group_size": "sub_group_size", "zero_prefetch_bucket_size": "prefetch_bucket_size",
+    "zero_param_persistence_threshold": "param_persistence_threshold",
+    "zero_model_persistence_threshold": "model_persistence_threshold",
+    "zero_max_live_parameters": "max_live_parameters", "zero_max_reuse_distance": "max_reuse_distance",
+    "zero_gather_16bit_weights_on_model_save": "gather_16bit_weights_on_model_save",
+    "zero_ignore_unused_parameters": "ignore_unused_parameters", "zero_legacy_stage1": "legacy_stage1",
+    "zero_round_robin_gradients": "round_robin_gradients", "zero_load_from_fp32_weights": "load_from_fp32_weights",
+    "zero_elastic_checkpoint": "elastic_checkpoint", "zero_hpz_partition_size": "zero_hpz_partition_size",
+    "zero_quantized_weights": "zero_quantized_weights", "zero_quantized_gradients": "zero_quantized_gradients",
+    "zero_quantized_nontrainable_weights": "zero_quantized_nontrainable_weights",
+}
+
+
+def _install_accessors():
+    def cfg_getter(attr):
+        return lambda self: getattr(self._config, attr)
+
+    def zero_getter(attr):
+        return lambda self: getattr(self._config.zero_config, attr)
+
+    for name, attr in _CONFIG_ACCESSORS.items():
+        if name not in DeepSpeedEngine.__dict__:
+            setattr(DeepSpeedEngine, name, cfg_getter(attr))
+    for name, attr in _ZERO_ACCESSORS.items():
+        if name not in DeepSpeedEngine.__dict__:
+            setattr(DeepSpeedEngine, name, zero_getter(attr))
+
+
+_install_accessors()
 
 _CKPT_KEYS = {
     "module", "buffer_names", "optimizer", "param_shapes", "frozen_param_shapes", "shared_params",

@@ -321,6 +321,46 @@ class PipelineEngine(DeepSpeedEngine):
             dist.broadcast(t, src=last, group=self.grid.get_pipe_parallel_group())
         return t[0]
 
+    def set_dataloader(self, loader):
+        """Stages that read data (first: inputs, last: labels) iterate `loader` (reference `pipe/engine.py:584`)."""
+        if self.is_first_stage() or self.is_last_stage():
+            self.training_dataloader = loader
+            self.data_iterator = iter(loader)
+
+    def set_has_attention_mask(self, value):
+        assert isinstance(value, bool)
+        self.has_attention_mask = value
+
+    def set_train_batch_size(self, train_batch_size):
+        """New global batch at the same micro-batch size: the number of micro-batches per step follows."""
+        super().set_train_batch_size(train_batch_size)
+        self.micro_batches = self.gradient_accumulation_steps()
+
+    def log_for_device(self, *msg):
+        if self.global_rank == 0:
+            logger.info(f"RANK={self.global_rank} PIPE-ID={self.stage_id} DATA-ID={self.grid.data_parallel_id} "
+                        + " ".join(str(m) for m in msg))
+
+    def mem_status(self, msg, print_rank=-1, reset_max=False):
+        """Device memory now / peak in GiB (reference `pipe/engine.py:1263-1300`)."""
+        if print_rank != -1 and self.global_rank != print_rank:
+            return
+        if self.device.type != "cuda":
+            return
+        torch.cuda.synchronize()
+        if reset_max:
+            torch.cuda.reset_peak_memory_stats()
+        gib = 1024**3
+        logger.info(f"RANK={self.global_rank} STAGE={self.stage_id} MEMSTATS {msg} "
+                    f"current alloc={torch.cuda.memory_allocated() / gib:.4f}GB "
+                    f"max alloc={torch.cuda.max_memory_allocated() / gib:.4f}GB "
+                    f"current cache={torch.cuda.memory_reserved() / gib:.4f}GB")
+
+    def tput_log(self, *msg):
+        if self.global_rank == 0 and self.tput_timer is not None:
+            logger.info(f"steps: {self.global_steps} samples/sec: {self.tput_timer.avg_samples_per_sec():.3f} "
+                        + " ".join(str(m) for m in msg))
+
     def forward(self, *args, **kwargs):
         raise RuntimeError("Only train_batch() / eval_batch() are accessible in pipeline mode.")
 

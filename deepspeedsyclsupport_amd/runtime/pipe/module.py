@@ -283,6 +283,14 @@ class PipelineModule(nn.Module):
     def num_pipeline_stages(self):
         return self.num_stages
 
+    def partitions(self):
+        """Stage boundaries over the layer list: stage s runs layers [parts[s], parts[s + 1])."""
+        return self.parts
+
+    def set_checkpoint_interval(self, interval):
+        assert interval >= 0
+        self.activation_checkpoint_interval = interval
+
     def ckpt_prefix(self, checkpoints_path, tag):
         return os.path.join(checkpoints_path, str(tag))
 

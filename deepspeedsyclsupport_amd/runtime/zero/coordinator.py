@@ -49,6 +49,9 @@ class ParamCoordinator:
         # ZeRO++ (qwZ quantized weight gather, hpZ intra-node secondary partitions)
         zc = opt.zc
         self.qwz = bool(zc is not None and zc.zero_quantized_weights)
+        # reference `zero_quantized_nontrainable_weights`: frozen weights travel as int8 blocks even when the trained
+        # ones are gathered in 16 bits
+        self.qnt = bool(zc is not None and zc.zero_quantized_nontrainable_weights)
         self.hpz = None
         if zc is not None and zc.zero_hpz_partition_size > 1 and opt.dp > zc.zero_hpz_partition_size:
             from ...parallel import groups
@@ -172,7 +175,7 @@ class ParamCoordinator:
             shard = staged
         if not g.partition:
             g.full.copy_(shard)
-        elif self.qwz:
+        elif self.qwz or (self.qnt and g.frozen):
             from .zeropp import quantized_all_gather
             quantized_all_gather(g.full, shard, g.dp_group)
         else:

@@ -162,6 +162,20 @@ class Init:
         if module is not None:
             self._convert(module)
 
+    def get_dp_process_group(self):
+        """The group parameters are partitioned over (reference `partition_parameters.py:968`)."""
+        return self.group
+
+    def get_partition_dp_group(self, param=None):
+        return getattr(param, "ds_process_group", self.group) if param is not None else self.group
+
+    def get_partition_rank(self):
+        return self.rank
+
+    @property
+    def num_partitions(self):
+        return self.dp
+
     def _convert(self, module):
         for m in module.modules():
             for p in m.parameters(recurse=False):

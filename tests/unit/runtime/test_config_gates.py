@@ -173,3 +173,47 @@ def test_fp16_auto_cast_inputs():
     x = {"a": torch.randn(2, 3), "b": [torch.arange(3), torch.randn(2, dtype=torch.float64)]}
     y = DeepSpeedEngine._cast_inputs_half(x)
     assert y["a"].dtype == torch.float16 and y["b"][0].dtype == torch.int64 and y["b"][1].dtype == torch.float16
+
+
+def _api(out):
+    import deepspeedsyclsupport_amd as ds
+    eng, *_ = ds.initialize(model=_net(), config=_cfg(zero_optimization={"stage": 2, "reduce_bucket_size": 12345},
+                                                      gradient_accumulation_steps=2))
+    res = {}
+    res["batch_info"] = eng.get_batch_info()
+    res["bucket"] = eng.zero_reduce_bucket_size()
+    res["names"] = (eng.optimizer_name(), eng.scheduler_name(), eng.zero_cpu_offload(), eng.zero_has_nvme_offload(),
+                    eng.dynamic_loss_scale(), eng.postscale_gradients(), eng.zero_quantized_nontrainable_weights())
+    res["types"] = [str(t) for t in eng.get_data_types()]
+    applied = []
+    g = torch.Generator().manual_seed(1)
+    for _ in range(4):
+        x, y = torch.randn(2, H, generator=g), torch.randint(0, 4, (2, ), generator=g)
+        eng.backward(nn.functional.cross_entropy(eng(x), y))
+        eng.step()
+        applied.append(eng.was_step_applied())
+    res["applied"] = applied
+    w = {k: v.clone() + 1.0 for k, v in eng.module.state_dict().items()}
+    eng.load_module_state_dict({"module": w})
+    res["loaded"] = all(torch.equal(v, w[k]) for k, v in eng.module.state_dict().items())
+    from deepspeedsyclsupport_amd.utils import safe_get_full_fp32_param
+    p = next(eng.module.parameters())
+    res["master_follows"] = bool(torch.equal(safe_get_full_fp32_param(p).cpu(), w["0.weight"]))
+    eng.set_train_micro_batch_size(4)
+    res["batch_info2"] = eng.get_batch_info()
+    eng.update_optimizer_step(7)
+    eng.empty_partition_cache()
+    eng.destroy()
+    torch.save(res, out)
+
+
+def test_engine_api_surface(tmp_path):
+    out = str(tmp_path / "r.pt")
+    run_distributed(_api, 1, out)
+    r = torch.load(out)
+    assert r["batch_info"] == (4, 2, 2) and r["batch_info2"] == (8, 4, 2)
+    assert r["bucket"] == 12345
+    assert r["names"] == ("adamw", None, False, False, True, True, False)
+    assert r["types"] == ["torch.float32", "torch.float32"]
+    assert r["applied"] == [False, True, False, True]
+    assert r["loaded"] and r["master_follows"]
