@@ -12,6 +12,9 @@ __git_branch__ = None
 
 import torch  # noqa: E402
 
+from . import _import_paths  # noqa: E402
+
+_import_paths.install()  # reference module paths that are folded into other files here
 from . import comm  # noqa: E402,F401
 from . import comm as dist  # noqa: E402,F401
 from .accelerator import get_accelerator  # noqa: E402,F401
@@ -21,6 +24,12 @@ from .runtime.config import DeepSpeedConfig, DeepSpeedConfigError  # noqa: E402,
 from .runtime.engine import DeepSpeedEngine  # noqa: E402,F401
 from .runtime.lr_schedules import add_tuning_arguments  # noqa: E402,F401
 from .utils.logging import log_dist, logger  # noqa: E402,F401
+
+# reference type aliases for the `optimizer=` / `lr_scheduler=` callables of `initialize`
+from typing import Callable, Iterable, Union  # noqa: E402
+
+DeepSpeedOptimizerCallable = Callable[[Union[Iterable[torch.nn.Parameter], dict]], torch.optim.Optimizer]
+DeepSpeedSchedulerCallable = Callable[[torch.optim.Optimizer], object]
 
 
 # the rest of the reference's top-level names, imported on first use (keeps `import` light and cycle-free)

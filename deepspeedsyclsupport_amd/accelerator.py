@@ -370,3 +370,8 @@ def set_accelerator(accel):
 @functools.lru_cache(None)
 def is_rocm_device():
     return isinstance(get_accelerator(), RocmAccelerator)
+
+
+# `deepspeed.accelerator.real_accelerator` is a sub-module path in the reference; this one-file accelerator answers it
+# through the package's import-path finder, for which the module must look like a package
+__path__ = []

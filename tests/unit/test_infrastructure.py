@@ -212,3 +212,24 @@ def test_aio_handle_round_trip(tmp_path):
     assert os.path.getsize(path) == (1 << 18) * 4
     h.free_cpu_locked_tensor(src)
     h.free_cpu_locked_tensor(dst)
+
+
+def test_reference_import_paths_resolve():
+    """Module paths of the reference that are folded into other files here still import (served by the package's
+    import-path finder) and hand out the real classes."""
+    import importlib
+
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import _import_paths
+    from deepspeedsyclsupport_amd.runtime.zero.flat_optimizer import FlatZeroOptimizer
+    for rel, targets in _import_paths.PATHS.items():
+        mod = importlib.import_module(f"deepspeedsyclsupport_amd.{rel}")
+        for _, names in targets:
+            if names != "*":
+                for exposed in names:
+                    assert hasattr(mod, exposed), (rel, exposed)
+    from deepspeedsyclsupport_amd.accelerator.real_accelerator import get_accelerator
+    from deepspeedsyclsupport_amd.runtime.zero.stage3 import DeepSpeedZeroOptimizer_Stage3
+    assert issubclass(DeepSpeedZeroOptimizer_Stage3, FlatZeroOptimizer) and get_accelerator is ds.get_accelerator
+    with pytest.raises(ModuleNotFoundError):
+        importlib.import_module("deepspeedsyclsupport_amd.runtime.zero.no_such_module")
