@@ -4,9 +4,10 @@
 // LayerNormBackward1/2) and inference `csrc/transformer/inference/csrc/{layer_norm.cu,rms_norm.cu}`
 // (fused_ln, fused_residual_ln, rms_norm, pre_rms_norm).
 //
-// MI355X design: ONE WAVE PER ROW. A 64-lane wave owns a row; forward keeps it in NV*8 registers per lane
-// (NV = compile-time vectors per lane, hidden <= 8192), so the statistics need only a 64-lane butterfly (no LDS, no
-// __syncthreads) and the row is read from HBM exactly once. 256-thread blocks = 4 rows; every access is 16 B/lane.
+// MI355X design: the backward kernels and the forward of narrow rows (< 1024) give ONE WAVE one row: it keeps the
+// row in NV*8 registers per lane (NV = compile-time vectors per lane), so the statistics need only a 64-lane
+// butterfly (no LDS, no __syncthreads) and the row is read from HBM exactly once; 256-thread blocks = 4 rows, every
+// access is 16 B/lane. The forward of wider rows gives a whole block one row (see norm_fwd_block_kernel).
 // Backward: pass 1 over the row accumulates the dot products and the per-lane dgamma/dbeta partials, pass 2
 // re-reads the (L1/L2-hot) row to write dx. dgamma/dbeta partials are reduced across the block's 4 waves in LDS
 // and written as one fp32 row per block, then summed by a column kernel (deterministic, no float atomics).
@@ -386,6 +387,88 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
+// ------------------------------------------------------------------------------------------------ wide-row forward
+// Rows of 1024 - 16384 elements: a 256-thread block owns the row, every thread holds NB <= 8 chunks, the statistics
+// go through the 64-lane butterfly and 4 LDS words. (With one wave per row a 14336-wide row is 28 dependent 16-B
+// loads per lane and a register file's worth of values: 35 us for ONE BLOOM-176B decode LayerNorm against 5.5 us
+// here, and 1.5 - 2.4x slower at training row counts.) LN = LayerNorm (mean + variance, gamma / beta), else RMSNorm.
+template <typename T, int NB, bool RES, bool LN>
+__global__ void __launch_bounds__(256) norm_fwd_block_kernel(const T* __restrict__ x, const T* __restrict__ r,
+                                                             const T* __restrict__ gamma, const T* __restrict__ beta,
+                                                             T* __restrict__ y, T* __restrict__ res_out,
+                                                             float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                             int H, float eps) {
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t row = blockIdx.x;
+  float v[NB][8];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int c = (k * 256 + tid) * 8;
+    if (c < H) {
+      Vec8<T>::load(x + row * H + c, v[k]);
+      if (RES) {
+        float rr[8];
+        Vec8<T>::load(r + row * H + c, rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += rr[j];
+        Vec8<T>::store(res_out + row * H + c, v[k]);
+      }
+    } else {
+      zero8(v[k]);
+    }
+  }
+  float mu = 0.f;
+  if (LN) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[k][j];
+    s = wave_sum(s);
+    if (lane == 0) red[0][wid] = s;
+    __syncthreads();
+    mu = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / H;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    if ((k * 256 + tid) * 8 < H) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[k][j] - mu;
+        ss = fmaf(d, d, ss);
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  if (lane == 0) red[1][wid] = ss;
+  __syncthreads();
+  const float rs = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / H + eps);
+  if (tid == 0) {
+    if (LN && mean_out) mean_out[row] = mu;
+    if (rstd_out) rstd_out[row] = rs;
+  }
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int c = (k * 256 + tid) * 8;
+    if (c < H) {
+      float gg[8], o[8];
+      Vec8<T>::load(gamma + c, gg);
+      if (LN) {
+        float bb[8];
+        Vec8<T>::load(beta + c, bb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mu) * rs * gg[j] + bb[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[k][j] * rs * gg[j];
+      }
+      Vec8<T>::store(y + row * H + c, o);
+    }
+  }
+}
+
 }  // namespace
 
 #define DISPATCH_T(dt, ...)                                    \
@@ -410,13 +493,31 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
 
 // forward-only buckets for very wide rows (BLOOM-176B: 14336): one wave still owns a whole row, up to 256 fp32
 // values per lane in registers (one wave per SIMD at that size; the row-per-wave structure avoids a block reduction)
-#define DISPATCH_NV_FWD(H, ...)                                  \
-  do {                                                           \
-    const int nvf__ = ((H) + 511) / 512;                         \
-    if (nvf__ <= 16) { DISPATCH_NV(H, __VA_ARGS__); }            \
-    else if (nvf__ <= 24) { constexpr int NV = 24; __VA_ARGS__; } \
-    else { constexpr int NV = 32; __VA_ARGS__; }                 \
+
+
+// Rows of 1024+ elements: a block per row at every row count (measured faster than a wave per row from 1 row to
+// 32768, 1.1x at hidden 4096 and 1.5 - 2.4x at 8192 / 14336); narrower rows keep the wave-per-row kernels.
+static bool block_rows(int H) { return H >= 1024; }
+
+template <typename T, bool LN>
+static void launch_block_norm(const void* x, const void* r, const void* g, const void* b, void* y, void* res_out,
+                              float* mean, float* rstd, int64_t rows, int H, float eps, hipStream_t s) {
+  const int nb = (H + 2047) / 2048;
+#define DS_BLOCK_NORM(NB_)                                                                                          \
+  do {                                                                                                              \
+    if (r)                                                                                                          \
+      hipLaunchKernelGGL((norm_fwd_block_kernel<T, NB_, true, LN>), dim3((unsigned)rows), dim3(256), 0, s,          \
+                         (const T*)x, (const T*)r, (const T*)g, (const T*)b, (T*)y, (T*)res_out, mean, rstd, H, eps); \
+    else                                                                                                            \
+      hipLaunchKernelGGL((norm_fwd_block_kernel<T, NB_, false, LN>), dim3((unsigned)rows), dim3(256), 0, s,         \
+                         (const T*)x, nullptr, (const T*)g, (const T*)b, (T*)y, nullptr, mean, rstd, H, eps);       \
   } while (0)
+  if (nb <= 1) DS_BLOCK_NORM(1);
+  else if (nb <= 2) DS_BLOCK_NORM(2);
+  else if (nb <= 4) DS_BLOCK_NORM(4);
+  else DS_BLOCK_NORM(8);
+#undef DS_BLOCK_NORM
+}
 
 static constexpr int kMaxHidden = 8192;      // backward kernels
 static constexpr int kMaxHiddenFwd = 16384;  // forward kernels
@@ -431,8 +532,13 @@ extern "C" int ds_rms_fwd(const void* x, const void* r, const void* w, void* y, 
   if (H % 8 != 0 || H > kMaxHiddenFwd) return (int)hipErrorInvalidValue;
   if (r && !res_out) return (int)hipErrorInvalidValue;  // the fused-residual kernel always writes x + r
   if (rows <= 0) return 0;
+  if (block_rows(H)) {
+    DISPATCH_T(dtype, (launch_block_norm<T, false>(x, r, w, nullptr, y, res_out, nullptr, rstd, rows, H, eps, s)));
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   const int grid = norm_grid(rows);
-  DISPATCH_T(dtype, DISPATCH_NV_FWD(H, {
+  DISPATCH_T(dtype, DISPATCH_NV(H, {
     if (r)
       hipLaunchKernelGGL((rms_fwd_kernel<T, NV, true>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)r,
                          (const T*)w, (T*)y, (T*)res_out, rstd, rows, H, eps);
@@ -469,8 +575,13 @@ extern "C" int ds_ln_fwd(const void* x, const void* r, const void* g, const void
   if (H % 8 != 0 || H > kMaxHiddenFwd) return (int)hipErrorInvalidValue;
   if (r && !res_out) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
+  if (block_rows(H)) {
+    DISPATCH_T(dtype, (launch_block_norm<T, true>(x, r, g, b, y, res_out, mean, rstd, rows, H, eps, s)));
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   const int grid = norm_grid(rows);
-  DISPATCH_T(dtype, DISPATCH_NV_FWD(H, {
+  DISPATCH_T(dtype, DISPATCH_NV(H, {
     if (r)
       hipLaunchKernelGGL((ln_fwd_kernel<T, NV, true>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)r,
                          (const T*)g, (const T*)b, (T*)y, (T*)res_out, mean, rstd, rows, H, eps);

@@ -25,7 +25,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build(layers, dev):
+def build(layers, dev, bits=8, group=64):
     from deepspeedsyclsupport_amd.inference.model_implementations.transformer import (DSInferenceModel, DSModelSpec,
                                                                                     alibi_slopes)
     spec = DSModelSpec(arch="bloom", vocab_size=250880, hidden_size=14336, num_layers=layers, num_heads=112,
@@ -58,7 +58,7 @@ def build(layers, dev):
                     p.fill_(1.0)
                 else:
                     p.zero_()
-        layer.quantize_weights(8, 64)
+        layer.quantize_weights(bits, group)
         if i % 10 == 0:
             log(f"[bloom] layer {i}/{layers} quantised, {torch.cuda.memory_allocated() / 2**30:.1f} GiB, "
                 f"{time.time() - t0:.1f}s")
@@ -73,16 +73,17 @@ def main():
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--gen", type=int, default=32)
     ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--bits", type=int, default=8, choices=(4, 8))
+    ap.add_argument("--group", type=int, default=64)
     args = ap.parse_args()
     from deepspeedsyclsupport_amd.inference.config import DeepSpeedInferenceConfig
     from deepspeedsyclsupport_amd.inference.engine import InferenceEngine
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    model, spec = build(args.layers, dev)
-    n_q = sum(layer.quant[n].i8.qsh.numel() if layer.quant[n].i8 is not None else layer.quant[n].qt.data.numel()
-              for layer in model.layers for n in layer.quant)
+    model, spec = build(args.layers, dev, args.bits, args.group)
+    n_q = sum(layer.quant[n].shape.numel() for layer in model.layers for n in layer.quant)
     weights_gib = torch.cuda.memory_allocated() / 2**30
-    log(f"[bloom] built: {n_q / 1e9:.1f}B int8 layer params + embedding, {weights_gib:.1f} GiB on device")
+    log(f"[bloom] built: {n_q / 1e9:.1f}B int{args.bits} layer params + embedding, {weights_gib:.1f} GiB on device")
     cfg = DeepSpeedInferenceConfig(dtype="bf16", enable_cuda_graph=bool(args.graph), max_tokens=args.prompt + args.gen)
     eng = InferenceEngine.from_ds_model(model, cfg)
     for B in [int(b) for b in args.batches.split(",")]:
@@ -99,7 +100,7 @@ def main():
         t_all = time.perf_counter() - t0
         dec = max(t_all - t_prefill, 1e-9) / (args.gen - 1)
         print(json.dumps({"model": "BLOOM-176B" if args.layers == 70 else f"BLOOM-176B-{args.layers}L",
-                          "weights": "int8 weight-only (group 64) + bf16 embedding", "n_gpus": 1, "tp": 1,
+                          "weights": f"int{args.bits} weight-only (group {args.group}) + bf16 embedding", "n_gpus": 1, "tp": 1,
                           "batch": B, "prompt": args.prompt, "gen": args.gen, "hip_graph": bool(args.graph),
                           "device_weights_gib": round(weights_gib, 1),
                           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
