@@ -42,6 +42,8 @@ struct Tile {
 #pragma unroll
     for (int m = 0; m < MM; ++m) acc[m][0] = acc[m][1] = 0.f;
   }
+  // `K` below is the END of the k-range being streamed (the whole row, or this wave's slice of it); `ldx` is the
+  // length of an activation row.
   __device__ __forceinline__ static void load(bf16x8 (&w0)[U], bf16x8 (&w1)[U], const bf16* r0, const bf16* r1,
                                               int base, int K, int lane) {
 #pragma unroll
@@ -57,7 +59,7 @@ struct Tile {
     }
   }
   __device__ __forceinline__ void fma(const bf16x8 (&w0)[U], const bf16x8 (&w1)[U], const bf16* xs, const bf16* xg,
-                                      int base, int K, int M, int lane) {
+                                      int base, int K, int ldx, int M, int lane) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int c = base + (u * 64 + lane) * 8;
@@ -68,7 +70,7 @@ struct Tile {
 #pragma unroll
       for (int m = 0; m < MM; ++m) {
         if (m >= M) break;  // wave-uniform
-        const bf16x8 xv = *reinterpret_cast<const bf16x8*>((XLDS ? xs : xg) + (int64_t)m * K + c);
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>((XLDS ? xs : xg) + (int64_t)m * ldx + c);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = (float)xv[j];
@@ -80,18 +82,27 @@ struct Tile {
   }
 };
 
-template <int MM, int IN, bool GATED, bool XLDS>
+// KS = 1: every wave owns a row pair. KS = WAVES: the workgroup owns ONE pair and its waves split the k-range (each
+// a contiguous quarter), partial sums meeting in LDS — for projections with few output rows (N = 4096: 512
+// workgroups at KS = 1, two per CU, each wave walking a 22 KB row serially; 2048 workgroups at KS = 4).
+template <int MM, int IN, bool GATED, bool XLDS, int KS>
 __global__ void __launch_bounds__(WAVES * 64) skinny_kernel(
     const bf16* __restrict__ W, const bf16* __restrict__ x, const bf16* __restrict__ r, const bf16* __restrict__ nw,
     const bf16* __restrict__ bias, const bf16* __restrict__ add, bf16* __restrict__ y, bf16* __restrict__ res_out,
     int M, int N, int K, float eps, int act) {
   extern __shared__ __attribute__((aligned(16))) bf16 xs[];  // [M][K] staged activations
   __shared__ float red[WAVES][MM];
+  __shared__ float part[WAVES][MM][2];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // this wave's k-range [k0, k1)
+  const int Kq = KS == 1 ? K : ((K / 8 + KS - 1) / KS) * 8;
+  const int k0 = KS == 1 ? 0 : min(K, wid * Kq);
+  const int k1 = KS == 1 ? K : min(K, k0 + Kq);
+  const int pstride = KS == 1 ? gridDim.x * WAVES : gridDim.x;
 
   // first weight tile of this wave's first pair: issued before staging X so HBM latency overlaps the staging
   const int pairs = GATED ? N / 2 : (N + 1) / 2;
-  int p = blockIdx.x * WAVES + wid;
+  int p = KS == 1 ? blockIdx.x * WAVES + wid : blockIdx.x;
   bf16x8 a0[U], a1[U], b0[U], b1[U];
   auto rows_of = [&](int pp, const bf16*& r0, const bf16*& r1, int& n0, int& n1) {
     n0 = GATED ? pp : 2 * pp;
@@ -103,7 +114,7 @@ __global__ void __launch_bounds__(WAVES * 64) skinny_kernel(
     const bf16 *r0, *r1;
     int n0, n1;
     rows_of(p, r0, r1, n0, n1);
-    Tile<MM, XLDS>::load(a0, a1, r0, r1, 0, K, lane);
+    Tile<MM, XLDS>::load(a0, a1, r0, r1, k0, k1, lane);
   }
 
   // ---------------------------------------------------------------- stage X (with the input-side fusion)
@@ -163,30 +174,59 @@ __global__ void __launch_bounds__(WAVES * 64) skinny_kernel(
   }
 
   // ---------------------------------------------------------------- stream weight-row pairs
-  for (bool first = true; p < pairs; p += gridDim.x * WAVES, first = false) {
+  for (bool first = true; p < pairs; p += pstride, first = false) {
     const bf16 *r0, *r1;
     int n0, n1;
     rows_of(p, r0, r1, n0, n1);
     Tile<MM, XLDS> t;
     t.zero();
-    if (!first) Tile<MM, XLDS>::load(a0, a1, r0, r1, 0, K, lane);
-    for (int base = 0; base < K; base += 2 * STEP) {
-      const bool more = base + STEP < K;
-      if (more) Tile<MM, XLDS>::load(b0, b1, r0, r1, base + STEP, K, lane);
-      t.fma(a0, a1, xs, x, base, K, M, lane);
+    if (!first) Tile<MM, XLDS>::load(a0, a1, r0, r1, k0, k1, lane);
+    for (int base = k0; base < k1; base += 2 * STEP) {
+      const bool more = base + STEP < k1;
+      if (more) Tile<MM, XLDS>::load(b0, b1, r0, r1, base + STEP, k1, lane);
+      t.fma(a0, a1, xs, x, base, k1, K, M, lane);
       if (more) {
-        if (base + 2 * STEP < K) Tile<MM, XLDS>::load(a0, a1, r0, r1, base + 2 * STEP, K, lane);
-        t.fma(b0, b1, xs, x, base + STEP, K, M, lane);
+        if (base + 2 * STEP < k1) Tile<MM, XLDS>::load(a0, a1, r0, r1, base + 2 * STEP, k1, lane);
+        t.fma(b0, b1, xs, x, base + STEP, k1, K, M, lane);
       }
     }
+    float s0[MM], s1[MM];
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
+      s0[m] = s1[m] = 0.f;
       if (m >= M) break;
-      const float s0 = wave_sum(t.acc[m][0]);
-      const float s1 = wave_sum(t.acc[m][1]);
+      s0[m] = wave_sum(t.acc[m][0]);
+      s1[m] = wave_sum(t.acc[m][1]);
+    }
+    if (KS > 1) {
+      // (the pair loop is uniform over the workgroup, so these barriers are reached by all of its waves)
       if (lane == 0) {
-        float o0 = s0 + (bias ? (float)bias[n0] : 0.f);
-        float o1 = s1 + (bias ? (float)bias[n1] : 0.f);
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+          part[wid][m][0] = s0[m];
+          part[wid][m][1] = s1[m];
+        }
+      }
+      __syncthreads();
+      if (wid == 0) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+          s0[m] = s1[m] = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) {
+            s0[m] += part[w][m][0];
+            s1[m] += part[w][m][1];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (lane == 0 && (KS == 1 || wid == 0)) {
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        if (m >= M) break;
+        float o0 = s0[m] + (bias ? (float)bias[n0] : 0.f);
+        float o1 = s1[m] + (bias ? (float)bias[n1] : 0.f);
         if (GATED) {
           const float g = (float)(bf16)o0, u = (float)(bf16)o1;  // HF rounds the projections to bf16 first
           const int Nh = N / 2;
@@ -216,13 +256,25 @@ int launch(const bf16* W, const bf16* x, const bf16* r, const bf16* nw, const bf
       g_cus = 256;
   }
   const int pairs = GATED ? N / 2 : (N + 1) / 2;
-  // one wave per row pair while that keeps the grid <= 8 workgroups per CU (dynamic dispatch balances the tail);
-  // beyond that the grid is persistent and waves stride over pairs
-  int grid = (pairs + WAVES - 1) / WAVES;
-  if (grid > 8 * g_cus) grid = 8 * g_cus;
   const size_t lds = XLDS ? (size_t)M * K * sizeof(bf16) : 0;
-  hipLaunchKernelGGL((skinny_kernel<MM, IN, GATED, XLDS>), dim3(grid), dim3(WAVES * 64), lds, s, W, x, r, nw, bias,
-                     add, y, res_out, M, N, K, eps, act);
+  // one wave per row pair while that keeps the grid <= 4 workgroups per CU; beyond that the grid is persistent and
+  // waves stride over pairs, so X is staged (and, with IN 1, normalised) once per resident workgroup instead of once
+  // per wave of workgroups (Llama-7B batch-1 decode 3.30 -> 3.15 ms/token against a cap of 8). Few pairs (< 4
+  // workgroups per CU that way): one pair per workgroup, its waves splitting the k-range. DS_SKINNY_CAP /
+  // DS_SKINNY_KS_WGS override the two thresholds for measurements.
+  static const int cap_env = [] { const char* e = getenv("DS_SKINNY_CAP"); return e ? atoi(e) : 0; }();
+  static const int ks_env = [] { const char* e = getenv("DS_SKINNY_KS_WGS"); return e ? atoi(e) : 4; }();
+  const int cap = (cap_env > 0 ? cap_env : 4) * g_cus;
+  int grid = (pairs + WAVES - 1) / WAVES;
+  if (grid < ks_env * g_cus && K >= 2048) {
+    grid = pairs > 8 * g_cus ? 8 * g_cus : pairs;
+    hipLaunchKernelGGL((skinny_kernel<MM, IN, GATED, XLDS, WAVES>), dim3(grid), dim3(WAVES * 64), lds, s, W, x, r, nw,
+                       bias, add, y, res_out, M, N, K, eps, act);
+  } else {
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL((skinny_kernel<MM, IN, GATED, XLDS, 1>), dim3(grid), dim3(WAVES * 64), lds, s, W, x, r, nw, bias,
+                       add, y, res_out, M, N, K, eps, act);
+  }
   DS_CHECK_LAUNCH();
   return 0;
 }
