@@ -80,6 +80,10 @@ class DeepSpeedInferenceConfig(DeepSpeedConfigModel):
     dtype: object = torch.float16
     tensor_parallel: DeepSpeedTPConfig = Field(DeepSpeedTPConfig(), alias="tp")
     enable_cuda_graph: bool = False
+    # bf16 projection weights for decode (`ops/bf16_gemv.py`): "row_major" = the parameters only; "both" = plus a
+    # copy in MFMA operand order for steps of 2 - 16 token rows (twice the weight memory); "shuffled" = operand
+    # order only (prefill un-shuffles per GEMM); "auto" = "both" when the copy fits in a quarter of the device memory
+    decode_layout: str = "auto"
     use_triton: bool = False
     triton_autotune: bool = False
     zero: DeepSpeedZeroConfig = DeepSpeedZeroConfig()

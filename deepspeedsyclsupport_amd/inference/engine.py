@@ -89,6 +89,8 @@ class InferenceEngine(torch.nn.Module):
             self.injected = True
             if config.quant.enabled and config.quant.weight.enabled:
                 self.module.quantize_weights(config.quant.weight.num_bits, config.quant.weight.group_size)
+            else:
+                self._apply_decode_layout(config)
             del model
         else:
             if self.tp_size > 1:
@@ -99,6 +101,25 @@ class InferenceEngine(torch.nn.Module):
                 self.module = self.module.to(self.dtype)
         self.module.eval()
         log_dist(f"InferenceEngine: injected={self.injected} tp={self.tp_size} dtype={self.dtype}", ranks=[0])
+
+    def _apply_decode_layout(self, config):
+        """`decode_layout` of the inference config: a shuffled copy of the bf16 projection weights for batched
+        decode when it is asked for, or ("auto") when it costs less than a quarter of the device memory."""
+        mode = getattr(config, "decode_layout", "auto")
+        m = self.module
+        if mode == "row_major" or self.dtype != torch.bfloat16 or self.device.type != "cuda" or self.tp_size != 1 \
+                or not hasattr(m, "add_decode_layout"):
+            return
+        if mode == "shuffled":
+            m.quantize_weights(16)
+            return
+        if mode == "auto":
+            total = torch.cuda.get_device_properties(self.device).total_memory
+            if m.projection_bytes() > total // 4:
+                return
+        n = m.add_decode_layout()
+        log_dist(f"InferenceEngine: {n} layers keep a shuffled decode copy of their projection weights "
+                 f"({m.projection_bytes() / 2**30:.1f} GiB extra)", ranks=[0])
 
     @classmethod
     def from_ds_model(cls, ds_model: DSInferenceModel, config: DeepSpeedInferenceConfig, tp_group=None, tp_size=1,

@@ -90,17 +90,26 @@ def alibi_slopes(n_heads):
 
 
 class QuantLinearWeight:
-    """Group-quantised weight (int8/int4). Symmetric int8 with K a multiple of 64 and int4 with K a multiple of 128
-    are kept in MFMA operand order for the decode streams (`ops/int8_gemv.py`, `ops/int4_gemv.py`; `i8` holds either);
-    everything else is dequantised into a temporary right before its GEMM."""
+    """Decode-layout weight. Group-quantised (int8 / int4): symmetric int8 with K a multiple of 64 and int4 with K a
+    multiple of 128 are kept in MFMA operand order for the decode streams (`ops/int8_gemv.py`, `ops/int4_gemv.py`);
+    everything else is dequantised into a temporary right before its GEMM. bits=16: the bf16 weight itself re-laid in
+    operand order (`ops/bf16_gemv.py`), with or without a row-major copy for prefill (`group_size` < 0: keep one).
+    `i8` holds whichever stream object applies."""
 
     def __init__(self, w, bits=8, group_size=64):
+        from ...ops.bf16_gemv import Bf16Weight
         from ...ops.int4_gemv import Int4Weight
         from ...ops.int8_gemv import Int8Weight
         from ...ops.quantizer import quantize
         self.shape = w.shape
         self.dtype = w.dtype
         self.i8 = None
+        if bits == 16:
+            if not Bf16Weight.supported(w):
+                raise ValueError(f"bf16 decode layout needs a bf16 [N, K] weight with K % 64 == 0, got {tuple(w.shape)}")
+            self.i8 = Bf16Weight(w, keep_row_major=group_size < 0)
+            self.qt = None
+            return
         if Int8Weight.supported(w, bits, group_size):
             self.i8 = Int8Weight(w, group_size)
         elif Int4Weight.supported(w, bits, group_size):
@@ -237,16 +246,35 @@ class DSInferenceLayer(nn.Module):
             self.coef_w = nn.Parameter(torch.empty(2, H, **kw), requires_grad=False)
             self.coef_b = nn.Parameter(torch.zeros(2, **kw), requires_grad=False)
         self.quant = {}
+        # bf16 weights ALSO held in the shuffled decode layout (name -> Bf16Weight), next to the row-major parameters:
+        # decode steps of SH_MIN_ROWS..16 token rows stream these, everything else uses the parameters
+        self.sh = {}
         # split (aliased) projections: name -> list of weights / biases applied side by side (hybrid engine shares
         # the training module's separate q/k/v and gate/up tensors instead of fusing copies)
         self.split_w, self.split_b = {}, {}
 
     # ------------------------------------------------------------------------------------------ helpers
     def quantize_weights(self, bits=8, group_size=64):
+        self.sh = {}
         for name in ("qkv_w", "o_w") + (() if self.spec.num_experts else ("fc1_w", "fc2_w")):
             self.quant[name] = QuantLinearWeight(getattr(self, name).data, bits, group_size)
             getattr(self, name).data = torch.empty(0, dtype=getattr(self, name).dtype,
                                                    device=getattr(self, name).device)
+
+    SH_MIN_ROWS = 2  # measured on Llama-2-7B: the row-major stream wins at 1 token row, the shuffled one from 2 up
+
+    def add_decode_layout(self):
+        """Keep a second copy of the four projection weights in MFMA operand order (`ops/bf16_gemv.py`): twice the
+        weight memory — 288 GB of HBM is sized for it — for up to 1.2x on batched decode steps (2 - 16 token rows). No-op
+        for quantised, split or non-bf16 weights."""
+        from ...ops.bf16_gemv import Bf16Weight
+        if self.quant or self.split_w or self.spec.num_experts:
+            return False
+        ws = {n: getattr(self, n) for n in ("qkv_w", "o_w", "fc1_w", "fc2_w")}
+        if not all(w.is_cuda and Bf16Weight.supported(w.data) for w in ws.values()):
+            return False
+        self.sh = {n: Bf16Weight(w.data) for n, w in ws.items()}
+        return True
 
     def _linear(self, x, name, bias=None):
         """x . W^T (+ bias). Int8 weight-only layers run `Int8Weight.linear`: at decode sizes (<= 16 token rows) the
@@ -444,16 +472,27 @@ class DSInferenceLayer(nn.Module):
         return down, res2
 
     # ------------------------------------------------------------------------------ weight-only decode fast path
-    def _quant_skinny_ok(self, h):
+    def _streams(self, h):
+        """{projection name: weight-stream object} serving this input through the un-finalized decode GEMVs, or None:
+        the quantised / shuffled-only weights, or the extra shuffled copies for SH_MIN_ROWS..16 token rows."""
         spec = self.spec
-        if not self.quant or self.split_w or spec.norm != "rms" or spec.parallel_residual or spec.num_experts \
-                or self.tp != 1:
-            return False
+        if (not self.quant and not self.sh) or self.split_w or spec.norm != "rms" or spec.parallel_residual \
+                or spec.num_experts or self.tp != 1:
+            return None
         from ...ops.int8_gemv import PendingAcc, raw_ok
+        names = ("qkv_w", "o_w", "fc1_w", "fc2_w")
+        if self.quant:
+            if not all(self.quant.get(n) is not None and self.quant[n].i8 is not None for n in names):
+                return None
+            q = {n: self.quant[n].i8 for n in names}
+            return q if isinstance(h, PendingAcc) or raw_ok(h) else None
         if isinstance(h, PendingAcc):
-            return True
-        return raw_ok(h) and all(self.quant.get(n) is not None and self.quant[n].i8 is not None
-                                 for n in ("qkv_w", "o_w", "fc1_w", "fc2_w"))
+            return self.sh
+        rows = h.numel() // h.shape[-1]
+        return self.sh if raw_ok(h) and rows >= self.SH_MIN_ROWS else None
+
+    def _quant_skinny_ok(self, h):
+        return self._streams(h) is not None
 
     def _forward_quant_skinny(self, h, residual, meta, cache, rope, alibi):
         """Decode (<= 16 token rows) over int8 / int4 weights: the four weight streams leave their sums in the fp32
@@ -463,7 +502,7 @@ class DSInferenceLayer(nn.Module):
         The block output is returned still pending: the next layer's input norm consumes it."""
         from ...ops.int8_gemv import PendingAcc
         from ...ops.transformer.functional import ACT_CODES
-        eps, q = self.spec.norm_eps, self.quant
+        eps, q = self.spec.norm_eps, self._streams(h)
         if isinstance(h, PendingAcc):
             normed, res1 = h.finalize_rms(residual, self.ln1_w, eps)
         elif residual is None:
@@ -471,14 +510,14 @@ class DSInferenceLayer(nn.Module):
         else:
             normed, res1 = self._norm(h, self.ln1_w, None, residual)
         # the fused QKV epilogue (RoPE + cache append) consumes the projection's sums straight from the workspace
-        attn = self._attend(q["qkv_w"].i8.raw(normed, self.qkv_b), meta, cache, rope, alibi)
-        normed2, res2 = q["o_w"].i8.raw(attn, self.o_b).finalize_rms(res1, self.ln2_w, eps)
-        up = q["fc1_w"].i8.raw(normed2, self.fc1_b)
+        attn = self._attend(q["qkv_w"].raw(normed, self.qkv_b), meta, cache, rope, alibi)
+        normed2, res2 = q["o_w"].raw(attn, self.o_b).finalize_rms(res1, self.ln2_w, eps)
+        up = q["fc1_w"].raw(normed2, self.fc1_b)
         if self.spec.gated_mlp:
             mid = up.finalize_gated(ACT_CODES[self.spec.act])
         else:
             mid = DF.bias_activation(up.finalize(), None, self.spec.act)
-        return q["fc2_w"].i8.raw(mid, self.fc2_b), res2
+        return q["fc2_w"].raw(mid, self.fc2_b), res2
 
     def forward(self, h, residual, meta, cache, rope, alibi):
         """Pre-norm block. Returns (block_output, residual) where the caller adds them (fused in the next norm)."""
@@ -809,5 +848,15 @@ class DSInferenceModel(nn.Module):
         return self._logits(x)
 
     def quantize_weights(self, bits=8, group_size=64):
+        """Weight-only int8 / int4 (`bits` 8 / 4), or bits=16: bf16 weights kept ONLY in the shuffled decode layout."""
         for layer in self.layers:
             layer.quantize_weights(bits, group_size)
+
+    def add_decode_layout(self):
+        """Second, shuffled copy of every layer's projection weights for batched decode (see the layer method);
+        returns the number of layers that took one."""
+        return sum(bool(layer.add_decode_layout()) for layer in self.layers)
+
+    def projection_bytes(self):
+        return sum(getattr(layer, n).numel() * getattr(layer, n).element_size()
+                   for layer in self.layers for n in ("qkv_w", "o_w", "fc1_w", "fc2_w") if hasattr(layer, n))

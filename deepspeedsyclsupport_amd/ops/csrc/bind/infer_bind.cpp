@@ -32,6 +32,10 @@ int ds_skinny_i8_mfma(const void*, const int8_t*, const float*, const void*, voi
                       hipStream_t);
 int64_t ds_skinny_i8_mfma_ws_floats(int);
 void ds_skinny_i8_tune(int, int, int);
+int ds_skinny_b16_mfma_ok(int, int);
+int ds_skinny_b16_mfma(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
+int ds_unshuffle_sh16(const void*, void*, int, int, hipStream_t);
+void ds_skinny_b16_tune(int, int);
 int ds_dequant_sh(const int8_t*, const float*, void*, int, int, int, hipStream_t);
 int ds_skinny_i8(const void*, const int8_t*, const float*, const void*, void*, int, int, int, int, hipStream_t);
 int ds_skinny_i4_mfma_ok(int, int, int);
@@ -400,6 +404,52 @@ Tensor skinny_q_raw(Tensor x, Tensor wq, Tensor ws_s, int64_t N, int64_t gs, int
   return ws.acc.narrow(0, 0, 16 * NP).view({16, NP});
 }
 
+// bf16 MFMA stream over the pre-shuffled weight (ops/bf16_gemv.py: preshuffle16): x [M, K] bf16 (M <= 16),
+// wsh bf16 [ceil(N/16), K/64, 2, 64, 8] -> y [M, N] bf16; `raw`: the un-finalized fp32 workspace view [16, NP] instead
+// (same contract as skinny_q_raw).
+Tensor skinny_b16_impl(Tensor x, Tensor wsh, OptT bias, int64_t N, bool raw) {
+  need(x, "x"); need(wsh, "wsh");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && wsh.scalar_type() == at::kBFloat16,
+              "skinny_b16: bf16 x [M, K] and bf16 shuffled weight");
+  const int64_t M = x.size(0), K = x.size(1), NB = (N + 15) / 16;
+  TORCH_CHECK(ds_skinny_b16_mfma_ok((int)M, (int)K) != 0, "skinny_b16: unsupported shape (M ", M, ", K ", K, ")");
+  TORCH_CHECK(wsh.numel() == NB * 16 * K && wsh.is_contiguous(), "skinny_b16: shuffled weight size");
+  TORCH_CHECK(NB * K < ((int64_t)1 << 40) && N < ((int64_t)1 << 31) / 16, "skinny_b16: matrix too large");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(wsh.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_b16: 16-B aligned x / weight");
+  const void* bp = nullptr;
+  if (!raw && bias.has_value() && bias->defined()) {
+    need(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kBFloat16, "skinny_b16: bias bf16 [N]");
+    bp = bias->data_ptr();
+  }
+  auto& ws = i8_workspace(x, N);
+  if (raw) {
+    check(ds_skinny_b16_mfma(x.data_ptr(), wsh.data_ptr(), nullptr, nullptr, ws.acc.data_ptr<float>(), (int)M, (int)N,
+                             (int)K, stream()), "skinny_b16 (raw)");
+    const int64_t NP = ds_skinny_i8_mfma_ws_floats((int)N) / 16;
+    return ws.acc.narrow(0, 0, 16 * NP).view({16, NP});
+  }
+  auto y = torch::empty({M, N}, x.options());
+  check(ds_skinny_b16_mfma(x.data_ptr(), wsh.data_ptr(), bp, y.data_ptr(), ws.acc.data_ptr<float>(), (int)M, (int)N,
+                           (int)K, stream()), "skinny_b16");
+  return y;
+}
+Tensor skinny_b16_sh(Tensor x, Tensor wsh, OptT bias, int64_t N) { return skinny_b16_impl(x, wsh, bias, N, false); }
+Tensor skinny_b16_raw(Tensor x, Tensor wsh, int64_t N) { return skinny_b16_impl(x, wsh, c10::nullopt, N, true); }
+bool skinny_b16_ok(int64_t M, int64_t K) { return ds_skinny_b16_mfma_ok((int)M, (int)K) != 0; }
+
+// pre-shuffled bf16 -> row-major bf16 [N, K]
+Tensor unshuffle_sh16(Tensor wsh, int64_t N) {
+  need(wsh, "wsh");
+  TORCH_CHECK(wsh.scalar_type() == at::kBFloat16 && wsh.dim() == 5 && wsh.is_contiguous(), "unshuffle_sh16: layout");
+  const int64_t K = wsh.size(1) * 64;
+  TORCH_CHECK(wsh.size(0) == (N + 15) / 16, "unshuffle_sh16: sizes");
+  auto w = torch::empty({N, K}, wsh.options());
+  check(ds_unshuffle_sh16(wsh.data_ptr(), w.data_ptr(), (int)N, (int)K, stream()), "unshuffle_sh16");
+  return w;
+}
+
 const void* opt_bf16(const OptT& t, int64_t numel, const char* what) {
   if (!t.has_value() || !t->defined()) return nullptr;
   need(*t, what);
@@ -509,6 +559,12 @@ void register_inference_ops(pybind11::module& m) {
         py::arg("p"), py::arg("wpc"), py::arg("rounds") = 0);
   m.def("dequant_sh4", &dequant_sh4);
   m.def("skinny_q_raw", &skinny_q_raw);
+  m.def("skinny_b16_ok", &skinny_b16_ok);
+  m.def("skinny_b16_sh", &skinny_b16_sh, py::arg("x"), py::arg("wsh"), py::arg("bias"), py::arg("N"));
+  m.def("skinny_b16_raw", &skinny_b16_raw);
+  m.def("unshuffle_sh16", &unshuffle_sh16);
+  m.def("skinny_b16_tune", [](int64_t cfg, int64_t wpc) { ds_skinny_b16_tune((int)cfg, (int)wpc); }, py::arg("cfg"),
+        py::arg("wpc") = 0);
   m.def("skinny_finalize_rms", &skinny_finalize_rms);
   m.def("skinny_finalize_gated", &skinny_finalize_gated);
   m.def("skinny_finalize", &skinny_finalize);

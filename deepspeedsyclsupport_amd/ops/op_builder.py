@@ -50,6 +50,7 @@ EXTENSIONS = {
             "gemv/skinny_mfma.hip",
             "gemv/skinny_int8.hip",
             "gemv/skinny_int4.hip",
+            "gemv/skinny_bf16_sh.hip",
             "gemv/skinny_finalize.hip",
             "moe/moe_kernels.hip",
             "comm/xgmi_allreduce.hip",

@@ -295,3 +295,53 @@ def test_int8_decode_gpu(kind):
     assert (l8 - l16).abs().max().item() < 0.05 * l16.abs().max().item() + 0.05
     g8 = e8.generate(ids, max_new_tokens=6)
     assert g8.shape == g16.shape
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["both", "shuffled", "auto"])
+@pytest.mark.parametrize("B", [1, 4, 16])
+def test_bf16_decode_layouts_gpu(layout, B):
+    """`decode_layout`: batched decode over the shuffled bf16 copies (2 - 16 token rows; "shuffled": every decode
+    step, prefill un-shuffling per GEMM) must follow the row-major engine — same greedy tokens, close logits — with
+    and without HIP graphs, and the layouts are really in place."""
+    import copy
+
+    import deepspeedsyclsupport_amd as ds
+    m = tiny("llama", H=256).eval()
+    ids = _ids(B=B, S=20).cuda()  # (prompts longer than 16 rows: prefill never takes the decode streams)
+    ref = ds.init_inference(copy.deepcopy(m), dtype=torch.bfloat16, replace_with_kernel_inject=True,
+                            decode_layout="row_major")
+    eng = ds.init_inference(copy.deepcopy(m), dtype=torch.bfloat16, replace_with_kernel_inject=True,
+                            decode_layout=layout)
+    engg = ds.init_inference(copy.deepcopy(m), dtype=torch.bfloat16, replace_with_kernel_inject=True,
+                             decode_layout=layout, enable_cuda_graph=True)
+    l0 = eng.module.layers[0]
+    assert not ref.module.layers[0].sh and not ref.module.layers[0].quant
+    if layout == "shuffled":
+        assert l0.quant and l0.qkv_w.numel() == 0
+    else:
+        assert l0.sh and l0.qkv_w.numel() > 0
+    g0 = ref.generate(ids, max_new_tokens=8)
+    lr = ref(g0[:, :-1]).logits[:, -1].float()
+    le = eng(g0[:, :-1]).logits[:, -1].float()
+    assert (le - lr).abs().max().item() < 0.03 * lr.abs().max().item() + 0.03
+    # one decode step from the same cache state, through the stream that this batch size selects
+    from deepspeedsyclsupport_amd.ops import bf16_gemv
+    calls = {"raw": 0}
+    orig = bf16_gemv.Bf16Weight.raw
+
+    def spy(self, x, bias=None):
+        calls["raw"] += 1
+        return orig(self, x, bias)
+
+    bf16_gemv.Bf16Weight.raw = spy
+    try:
+        g1 = eng.generate(ids, max_new_tokens=8)
+    finally:
+        bf16_gemv.Bf16Weight.raw = orig
+    expect_stream = layout == "shuffled" or B >= l0.SH_MIN_ROWS
+    assert (calls["raw"] > 0) == expect_stream
+    g2 = engg.generate(ids, max_new_tokens=8)
+    assert torch.equal(g1, g2)
+    # greedy decoding may legitimately diverge after a near-tie; the first new token comes from the prefill logits
+    assert torch.equal(g1[:, :21], g0[:, :21]) or (le - lr).abs().max().item() < 0.05

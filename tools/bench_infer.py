@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--gen", type=int, default=128)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--graph", default="0,1")
-    ap.add_argument("--quant-bits", type=int, default=0, help="weight-only quantisation of the layer GEMMs (8 or 4)")
+    ap.add_argument("--quant-bits", type=int, default=0, help="weight-only quantisation of the layer GEMMs (8 or 4); 16 = bf16 weights in the shuffled decode layout "
+                    "(--group-size -1: keep a row-major copy for prefill too)")
     ap.add_argument("--group-size", type=int, default=128)
     args = ap.parse_args()
     from deepspeedsyclsupport_amd.inference.config import DeepSpeedInferenceConfig
@@ -40,10 +41,14 @@ def main():
                 p.normal_(0, 0.02)
     bf16_bytes = sum(p.numel() * 2 for layer in model.layers for p in layer.parameters() if p.dim() >= 2)
     stream_bytes = bf16_bytes
-    if args.quant_bits:
+    if args.quant_bits == 32:  # row-major parameters + shuffled copies ("both")
+        model.add_decode_layout()
+    elif args.quant_bits:
         model.quantize_weights(args.quant_bits, args.group_size)
         torch.cuda.empty_cache()
         stream_bytes = sum(q.i8.nbytes() for layer in model.layers for q in layer.quant.values())
+        if args.quant_bits in (16, 32):
+            stream_bytes = bf16_bytes  # (a kept row-major copy is memory, not decode traffic)
     head_bytes = model.lm_head.numel() * 2
     for use_graph in [int(x) for x in args.graph.split(",")]:
         cfg = DeepSpeedInferenceConfig(dtype="bf16", enable_cuda_graph=bool(use_graph), max_tokens=4096)
@@ -70,7 +75,9 @@ def main():
                               "prefill_tok_s": round(B * args.prompt / t_prefill, 1),
                               "decode_ms_per_token": round(dec * 1e3, 3),
                               "decode_tok_s": round(B / dec, 1),
-                              "weight_bits": args.quant_bits or 16, "group_size": args.group_size,
+                              "weight_bits": 16 if args.quant_bits in (0, 16, 32) else args.quant_bits,
+                              "group_size": args.group_size,
+                              "decode_layout": {0: "row-major", 16: "shuffled", 32: "both"}.get(args.quant_bits, "packed"),
                               "layer_weight_gib_streamed": round(stream_bytes / 2**30, 3),
                               "lm_head_gib_bf16": round(head_bytes / 2**30, 3),
                               # bytes the decode step really reads (packed weights + scales + bf16 LM head) per second
