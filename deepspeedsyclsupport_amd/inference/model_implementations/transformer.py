@@ -801,6 +801,13 @@ class DSInferenceModel(nn.Module):
         rope = (self.rope_cos, self.rope_sin)
         for layer in self.layers:
             h, residual = layer(h, residual, meta, self.cache, rope, self.alibi)
+        sh = getattr(self, "lm_head_sh", None)
+        if sh is not None and not all_logits and hasattr(h, "finalize_rms") and len(h.lead) == 2 and h.lead[1] == 1 \
+                and self.spec.final_norm and self.spec.norm == "rms":
+            # decode step over the shuffled copies: the last block's sums go through the fused residual + final
+            # RMSNorm finalize, then the LM head streams in operand order like every other projection
+            normed, _ = h.finalize_rms(residual, self.norm_w, self.spec.norm_eps)
+            return self._gather_vocab(sh.linear(normed[:, -1], self.lm_head_b))
         h = materialize(h)
         if not all_logits:
             h = h[:, -1].contiguous()
@@ -855,7 +862,11 @@ class DSInferenceModel(nn.Module):
     def add_decode_layout(self):
         """Second, shuffled copy of every layer's projection weights for batched decode (see the layer method);
         returns the number of layers that took one."""
-        return sum(bool(layer.add_decode_layout()) for layer in self.layers)
+        n = sum(bool(layer.add_decode_layout()) for layer in self.layers)
+        from ...ops.bf16_gemv import Bf16Weight
+        if n and self.tp_size == 1 and self.lm_head.is_cuda and Bf16Weight.supported(self.lm_head.data):
+            self.lm_head_sh = Bf16Weight(self.lm_head.data)  # the LM head streams every decode step too
+        return n
 
     def projection_bytes(self):
         return sum(getattr(layer, n).numel() * getattr(layer, n).element_size()
