@@ -107,7 +107,9 @@ def _train(out, use_init, zero_extra, steps=3):
     w = {n: safe_get_full_fp32_param(p).cpu() for n, p in m.named_parameters()}
     with ds.zero.GatheredParameters(frozen):
         assert all(p.numel() > 0 for p in frozen)
+    full = eng.consolidated_16bit_state_dict()  # the 16-bit export gathers trained and frozen groups alike
     if dist.get_rank() == 0:
+        assert set(full) == set(w) and all(torch.equal(full[n].float(), w[n]) for n in w)
         torch.save({"losses": losses, "w": w}, out)
 
 
@@ -209,3 +211,44 @@ def test_exclude_frozen_parameters_on_save(tmp_path):
             assert torch.equal(loaded["w"][n], init[n]), n      # not in the checkpoint: the model's own values stay
         else:
             assert torch.equal(loaded["w"][n], saved["w"][n]), n
+
+
+def _qnt(out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.runtime.zero import zeropp
+    calls = {"n": 0, "frozen_only": True}
+    orig = zeropp.quantized_all_gather
+
+    def spy(full, shard, group):
+        calls["n"] += 1
+        return orig(full, shard, group)
+
+    zeropp.quantized_all_gather = spy
+    m = freeze(build())
+    eng, *_ = ds.initialize(model=m, config=cfg(zero_quantized_nontrainable_weights=True),
+                            model_parameters=[p for p in m.parameters() if p.requires_grad])
+    losses = []
+    for x, y in data(3, dist.get_rank()):
+        loss = nn.functional.cross_entropy(eng(x), y)
+        eng.backward(loss)
+        eng.step()
+        t = loss.detach().clone()
+        dist.all_reduce(t)
+        losses.append(float(t) / dist.get_world_size())
+    n_frozen_fetches = sum(1 for g in eng.optimizer.frozen_groups)
+    if dist.get_rank() == 0:
+        torch.save({"losses": losses, "calls": calls["n"], "frozen_groups": n_frozen_fetches}, out)
+
+
+def test_quantized_nontrainable_weights_gather(tmp_path):
+    """`zero_quantized_nontrainable_weights`: only the frozen groups travel as int8 blocks; training follows the
+    16-bit run within quantisation noise."""
+    out = str(tmp_path / "r.pt")
+    run_distributed(_qnt, 2, out)
+    r = torch.load(out)
+    ref, _ = _reference(2, 3)
+    assert r["calls"] >= r["frozen_groups"] * 3          # every step fetches every frozen group at least once
+    assert r["calls"] <= r["frozen_groups"] * 3 * 2      # ... and only those (forward + backward fetches)
+    assert r["losses"] == pytest.approx(ref, rel=0.05, abs=0.05)
+    assert r["losses"] != pytest.approx(ref, rel=1e-7, abs=1e-9)
