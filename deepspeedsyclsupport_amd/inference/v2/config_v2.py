@@ -49,3 +49,5 @@ class RaggedInferenceEngineConfig(DeepSpeedConfigModel):
     kv_cache: KVCacheConfig = KVCacheConfig()
     quantization: QuantizationConfig = QuantizationConfig()
     enable_cuda_graph: bool = False
+    # bf16 projection weights for small ragged batches (<= 16 tokens), see `DeepSpeedInferenceConfig.decode_layout`
+    decode_layout: str = "auto"

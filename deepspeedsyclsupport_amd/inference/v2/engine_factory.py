@@ -39,7 +39,19 @@ def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = 
     q = engine_config.quantization.quantization_mode
     if q in ("int8", "int4"):
         ds_model.quantize_weights(8 if q == "int8" else 4)
+    else:
+        _apply_decode_layout(ds_model, engine_config.decode_layout, tp, device)
     return InferenceEngineV2(ds_model, engine_config)
+
+
+def _apply_decode_layout(ds_model, mode, tp, device):
+    """Same policy as `InferenceEngine._apply_decode_layout` (a shuffled copy of the bf16 projection weights)."""
+    if mode == "row_major" or tp != 1 or device.type != "cuda" or ds_model.dtype != torch.bfloat16:
+        return
+    if mode == "shuffled":
+        ds_model.quantize_weights(16)
+    elif mode == "both" or ds_model.projection_bytes() <= torch.cuda.get_device_properties(device).total_memory // 4:
+        ds_model.add_decode_layout()
 
 
 def build_engine_from_ds_checkpoint(path, engine_config: RaggedInferenceEngineConfig = None, debug_level=0,
@@ -81,4 +93,9 @@ def build_engine_from_ds_checkpoint(path, engine_config: RaggedInferenceEngineCo
     if unexpected or any(not k.startswith(("rope_", "alibi")) for k in missing):
         raise ValueError(f"serialized weights do not match the spec: missing {missing[:4]}, unexpected "
                          f"{unexpected[:4]}")
+    q = engine_config.quantization.quantization_mode
+    if q in ("int8", "int4"):
+        model.quantize_weights(8 if q == "int8" else 4)
+    else:
+        _apply_decode_layout(model, engine_config.decode_layout, tp, device)
     return InferenceEngineV2(model, engine_config)
