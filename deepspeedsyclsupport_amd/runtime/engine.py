@@ -421,6 +421,12 @@ class DeepSpeedEngine(nn.Module):
         if cfg.mics_hierarchial_params_gather:
             log_dist("mics_hierarchical_params_gather: MiCS shard groups are laid inside one xGMI node, where a single "
                      "all-gather already uses every link; the two-level gather is not used", ranks=[0])
+        for key, default in (("round_robin_gradients", False), ("legacy_stage1", False),
+                             ("pipeline_loading_checkpoint", False), ("use_multi_rank_bucket_allreduce", True),
+                             ("allgather_partitions", True), ("contiguous_gradients", True)):
+            if getattr(zc, key, default) != default:
+                log_dist(f"zero_optimization.{key}={getattr(zc, key)}: no effect here (gradients always live in "
+                         "contiguous flat buffers reduced per group; partitions are gathered per group)", ranks=[0])
         if cfg.graph_harvesting:
             log_dist("graph_harvesting: the gradient-norm and clipping passes are already single multi-tensor "
                      "launches (sumsq_multi, clip folded into the Adam kernel's gradient scale); nothing to capture",
@@ -1003,7 +1009,13 @@ class DeepSpeedEngine(nn.Module):
                 osd = self.checkpoint_engine.load(zpath, map_location="cpu")["optimizer_state_dict"]
             if osd is not None and CK.FLAT_LAYOUT in osd and \
                     zc.layouts_match(osd[CK.FLAT_LAYOUT], self.optimizer.layout()):
-                self.optimizer.load_state_dict(osd, load_optimizer_states=with_states)
+                # `load_from_fp32_weights: false` (reference `stage_1_and_2.py:2280-2310`): the masters are re-derived
+                # from the 16-bit module weights of the checkpoint instead of its fp32 partitions; under ZeRO-3 the
+                # module file holds placeholders, so the fp32 shards are the only source
+                from_fp32 = bool(self._config.zero_config.load_from_fp32_weights) or self._zero3_partitioned()
+                self.optimizer.load_state_dict(osd, load_optimizer_states=with_states, load_from_fp32_weights=from_fp32)
+                if not from_fp32:
+                    self.optimizer.refresh_from_module()
             elif zc.optim_files(tag_dir):
                 src = zc.open_source(tag_dir, 0 if self.mpu is None else self.mpu.get_model_parallel_rank())
                 log_dist(f"load_checkpoint: re-partitioning {type(src).__name__} ({len(src.files)} shard files) "
@@ -1262,7 +1274,13 @@ class DeepSpeedEngine(nn.Module):
 
 
     def save_16bit_model(self, save_dir, save_filename="pytorch_model.bin", exclude_frozen_parameters=False):
-        """Consolidated 16-bit weights, streamed group by group to rank 0 (reference `runtime/engine.py:3477`)."""
+        """Consolidated 16-bit weights, streamed group by group to rank 0 (reference `runtime/engine.py:3477`). As in
+        the reference (`engine.py:3618-3626`) a ZeRO-3 partitioned model is only gathered when
+        `stage3_gather_16bit_weights_on_model_save` allows it."""
+        if self._zero3_partitioned() and not self._config.zero_config.gather_16bit_weights_on_model_save:
+            logger.info(f"Did not save the model {os.path.join(save_dir, save_filename)} because "
+                        "`stage3_gather_16bit_weights_on_model_save` is False")
+            return False
         sd = self.consolidated_16bit_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
         if dist.get_rank() == 0:
             os.makedirs(save_dir, exist_ok=True)

@@ -26,6 +26,7 @@ MI355X-first design (why it is not a port):
   non-blocking copies on a side stream.
 """
 import math
+import sys
 import os
 from collections import OrderedDict, defaultdict
 
@@ -195,8 +196,16 @@ class FlatZeroOptimizer(ZeROOptimizer):
                                             getattr(ds_config, "dynamic_loss_scale_args", None))
         self.dynamic_loss_scale = self.loss_scaler.dynamic
         # streams
-        self.rs_stream = self.acc.Stream() if self.device.type == "cuda" else None
-        self.ag_stream = self.acc.Stream() if self.device.type == "cuda" else None
+        # side streams for the gradient reduce-scatter and the parameter all-gather: on unless the config says
+        # `overlap_comm: false` in so many words (the key's unset default differs per stage in the reference; here
+        # overlapping is the default for every stage)
+        zc_set = getattr(self.zc, "model_fields_set", set()) if self.zc is not None else set()
+        overlap = not ("overlap_comm" in zc_set and not self.zc.overlap_comm)
+        self.rs_stream = self.acc.Stream() if self.device.type == "cuda" and overlap else None
+        self.ag_stream = self.acc.Stream() if self.device.type == "cuda" and overlap else None
+        # `reduce_scatter: false` (reference stage 1/2): all-reduce the whole bucket and keep the owner's slice
+        self.use_reduce_scatter = bool(getattr(self.zc, "reduce_scatter", True)) if self.zc is not None else True
+        self.ignore_unused = bool(getattr(self.zc, "ignore_unused_parameters", True)) if self.zc is not None else True
         self._fused_adam = isinstance(self.optimizer, FusedAdam) or getattr(self.optimizer, "_ds_flat_adam", False)
         self._build_groups()
         self._build_master()
@@ -245,6 +254,7 @@ class FlatZeroOptimizer(ZeROOptimizer):
             thr = self.zc.param_persistence_threshold if fetched else 0
             owned = set()
             persistent = []
+            budget = int(getattr(self.zc, "model_persistence_threshold", sys.maxsize) or sys.maxsize)
             for name, m in self.module.named_modules():
                 ps = [p for p in m.parameters(recurse=False) if id(p) in self.param_to_og and id(p) not in owned]
                 if not ps:
@@ -254,8 +264,12 @@ class FlatZeroOptimizer(ZeROOptimizer):
                 for p in [p for p in ps if id(p) in self.sparse_params]:  # sparse-reduced weights: a group each
                     groups.append(dict(params=[p], persistent=not fetched, module=m, sparse=True))
                 ps = [p for p in ps if id(p) not in self.sparse_params]
-                big = [p for p in ps if _pnumel(p) >= thr]
-                small = [p for p in ps if _pnumel(p) < thr]
+                small = []
+                for p in ps:  # small parameters stay gathered while their total fits model_persistence_threshold
+                    if _pnumel(p) < thr and _pnumel(p) <= budget:
+                        small.append(p)
+                        budget -= _pnumel(p)
+                big = [p for p in ps if not any(p is q for q in small)]
                 persistent.extend(small)
                 if big:
                     big.sort(key=lambda p: self.param_to_og[id(p)])
@@ -674,6 +688,9 @@ class FlatZeroOptimizer(ZeROOptimizer):
             elif getattr(g, "sparse", False) and g.reduce_dp > 1:
                 comm = self._sparse_reduce(g, comm)
                 out = comm[g.seg_lo:g.seg_lo + g.seg]
+            elif g.partition and not self.use_reduce_scatter and self.mics_replica_group is None:
+                dist.all_reduce(comm, group=g.dp_group)
+                out = comm[g.seg_lo:g.seg_lo + g.seg]
             elif g.partition:
                 out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
                 if self.zc is not None and self.zc.zero_quantized_gradients:
@@ -745,6 +762,18 @@ class FlatZeroOptimizer(ZeROOptimizer):
     @instrument_w_nvtx
     def backward_epilogue(self):
         """Flush groups whose params got no grad this pass (unused params count as zero) and join streams."""
+        if not self.ignore_unused:
+            names = None
+            for g in self.groups:
+                if g.pending > 0:
+                    if names is None:
+                        names = {id(p): n for n, p in self.module.named_parameters()}
+                    missing = [names.get(id(p), "?") for p in g.params if p.grad is None and g.mode == self.LOCAL] \
+                        or [names.get(id(p), "?") for p in g.params][:g.pending]
+                    from .utils import ZeRORuntimeException
+                    raise ZeRORuntimeException(
+                        f"{g.pending} parameter(s) of fetch group {g.idx} received no gradient in this backward pass "
+                        f"(e.g. {missing[:3]}) and zero_optimization.ignore_unused_parameters is false")
         if self._should_reduce_now():
             for g in self.groups:
                 if g.mode != self.LOCAL and not g.reduced_this_pass:

@@ -136,7 +136,10 @@ def _consolidate(ckpt_dir, out):
     largest_group = max(g.padded for g in opt.groups)
     assert biggest["n"] <= largest_group, (biggest["n"], largest_group)
     ref = {n: safe_get_full_fp32_param(p) for n, p in eng.module.named_parameters()}
-    eng.save_16bit_model(ckpt_dir)
+    # as in the reference, the gathered export needs stage3_gather_16bit_weights_on_model_save
+    assert eng.save_16bit_model(ckpt_dir) is False and not os.path.exists(os.path.join(ckpt_dir, "pytorch_model.bin"))
+    eng._config.zero_config.gather_16bit_weights_on_model_save = True
+    assert eng.save_16bit_model(ckpt_dir) is True
     if rank == 0:
         assert set(sd) >= set(ref)
         for n, v in ref.items():

@@ -217,3 +217,69 @@ def test_engine_api_surface(tmp_path):
     assert r["types"] == ["torch.float32", "torch.float32"]
     assert r["applied"] == [False, True, False, True]
     assert r["loaded"] and r["master_follows"]
+
+
+def _zero_keys(out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.runtime.zero.utils import ZeRORuntimeException
+    res = {}
+    # reduce_scatter: false -> all-reduce + slice; same numbers as the reduce-scatter run
+    runs = {}
+    for rs in (True, False):
+        eng, *_ = ds.initialize(model=_net(), config=_cfg(zero_optimization={"stage": 2, "reduce_scatter": rs,
+                                                                             "overlap_comm": False}))
+        calls = {"rs": 0, "ar": 0}
+        o_rs, o_ar = dist.reduce_scatter_tensor, dist.all_reduce
+
+        def c_rs(*a, **k):
+            calls["rs"] += 1
+            return o_rs(*a, **k)
+
+        def c_ar(*a, **k):
+            calls["ar"] += 1
+            return o_ar(*a, **k)
+
+        dist.reduce_scatter_tensor, dist.all_reduce = c_rs, c_ar
+        losses = _steps(eng, 3, seed=3 + dist.get_rank())
+        dist.reduce_scatter_tensor, dist.all_reduce = o_rs, o_ar
+        runs[rs] = (losses, dict(calls), eng.optimizer.rs_stream is None)
+    res["runs"] = runs
+    # ignore_unused_parameters: false -> a parameter that gets no gradient is an error
+    class Unused(nn.Module):
+
+        def __init__(self):
+            super().__init__()
+            self.a, self.b = nn.Linear(H, 4), nn.Linear(H, 4)
+
+        def forward(self, x):
+            return self.a(x)
+
+    eng, *_ = ds.initialize(model=Unused(), config=_cfg(zero_optimization={"stage": 2,
+                                                                           "ignore_unused_parameters": False}))
+    x, y = torch.randn(2, H), torch.randint(0, 4, (2, ))
+    try:
+        eng.backward(nn.functional.cross_entropy(eng(x), y))
+        res["unused_raised"] = False
+    except ZeRORuntimeException as e:
+        res["unused_raised"] = "ignore_unused_parameters" in str(e)
+    # model_persistence_threshold caps what stays gathered under ZeRO-3
+    for cap in (None, 40):
+        z = {"stage": 3, "stage3_param_persistence_threshold": 1000}
+        if cap is not None:
+            z["stage3_model_persistence_threshold"] = cap
+        eng, *_ = ds.initialize(model=_net(), config=_cfg(zero_optimization=z))
+        res[f"persistent_{cap}"] = sum(g.numel for g in eng.optimizer.groups if g.persistent)
+    if dist.get_rank() == 0:
+        torch.save(res, out)
+
+
+def test_zero_keys_change_behaviour(tmp_path):
+    out = str(tmp_path / "r.pt")
+    run_distributed(_zero_keys, 2, out)
+    r = torch.load(out)
+    (l1, c1, nostream1), (l0, c0, nostream0) = r["runs"][True], r["runs"][False]
+    assert l1 == pytest.approx(l0, rel=1e-6) and c1["rs"] > 0 and c0["rs"] == 0 and c0["ar"] > c1["ar"]
+    assert nostream1 and nostream0       # overlap_comm: false was spelled out (no side streams on CPU anyway)
+    assert r["unused_raised"]
+    assert r["persistent_40"] < r["persistent_None"] and r["persistent_40"] <= 40 + 16
