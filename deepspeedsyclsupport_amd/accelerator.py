@@ -71,6 +71,76 @@ class _Base:
     def op_builder_dir(self):
         return "deepspeedsyclsupport_amd.ops"
 
+    # ------------------------------------------------------------------ op builders (reference
+    # `accelerator/abstract_accelerator.py:249-266`): one in-tree builder table serves every name
+    def get_op_builder(self, class_name):
+        from .ops import op_builder
+        return getattr(op_builder, class_name, None)
+
+    def create_op_builder(self, class_name):
+        cls = self.get_op_builder(class_name)
+        return None if cls is None else cls()
+
+    def build_extension(self):
+        from torch.utils.cpp_extension import BuildExtension
+        return BuildExtension
+
+    def export_envs(self):
+        """Environment variable prefixes the launcher forwards to remote ranks."""
+        return ["NCCL", "RCCL", "HSA", "HIP", "ROCR", "GPU_", "PYTORCH_"]
+
+    def is_triton_supported(self):
+        return False  # no Triton path in this framework: every kernel is in-tree HIP
+
+    def random(self):
+        return torch.random
+
+    def amp(self):
+        return getattr(torch, "amp", None)
+
+    # ------------------------------------------------------------------ legacy tensor constructors
+    def _tensor_type(self, dtype):
+        import functools
+        return functools.partial(torch.tensor, dtype=dtype, device=self.current_device_name())
+
+    @property
+    def BFloat16Tensor(self):
+        return self._tensor_type(torch.bfloat16)
+
+    @property
+    def ByteTensor(self):
+        return self._tensor_type(torch.uint8)
+
+    @property
+    def DoubleTensor(self):
+        return self._tensor_type(torch.float64)
+
+    @property
+    def FloatTensor(self):
+        return self._tensor_type(torch.float32)
+
+    @property
+    def HalfTensor(self):
+        return self._tensor_type(torch.float16)
+
+    @property
+    def IntTensor(self):
+        return self._tensor_type(torch.int32)
+
+    @property
+    def LongTensor(self):
+        return self._tensor_type(torch.int64)
+
+    # ------------------------------------------------------------------ older memory-stat names
+    def memory_cached(self, device_index=None):
+        return self.memory_reserved(device_index)
+
+    def max_memory_cached(self, device_index=None):
+        return self.max_memory_reserved(device_index)
+
+    def reset_max_memory_cached(self, device_index=None):
+        return self.reset_peak_memory_stats(device_index)
+
 
 class RocmAccelerator(_Base):
     """MI355X (gfx950) through PyTorch-ROCm: `torch.cuda` is the HIP runtime, `nccl` is RCCL."""

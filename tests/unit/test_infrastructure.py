@@ -233,3 +233,18 @@ def test_reference_import_paths_resolve():
     assert issubclass(DeepSpeedZeroOptimizer_Stage3, FlatZeroOptimizer) and get_accelerator is ds.get_accelerator
     with pytest.raises(ModuleNotFoundError):
         importlib.import_module("deepspeedsyclsupport_amd.runtime.zero.no_such_module")
+
+
+def test_accelerator_builder_and_legacy_surface():
+    """Names of the reference accelerator ABC that integrations call (`accelerator/abstract_accelerator.py`): op
+    builder lookup, legacy tensor constructors, older memory-stat names."""
+    import torch
+
+    from deepspeedsyclsupport_amd.accelerator import get_accelerator
+    a = get_accelerator()
+    b = a.create_op_builder("FusedAdamBuilder")
+    assert b is not None and type(b) is a.get_op_builder("FusedAdamBuilder") and a.get_op_builder("NoSuchBuilder") is None
+    assert a.FloatTensor([1, 2]).dtype == torch.float32 and a.HalfTensor([1]).dtype == torch.float16
+    assert a.LongTensor([1]).dtype == torch.int64 and a.BFloat16Tensor([1]).dtype == torch.bfloat16
+    assert a.memory_cached() == a.memory_reserved() and a.max_memory_cached() == a.max_memory_reserved()
+    assert a.amp() is torch.amp and not a.is_triton_supported() and "RCCL" in a.export_envs()
