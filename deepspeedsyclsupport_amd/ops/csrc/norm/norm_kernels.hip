@@ -4,10 +4,10 @@
 // LayerNormBackward1/2) and inference `csrc/transformer/inference/csrc/{layer_norm.cu,rms_norm.cu}`
 // (fused_ln, fused_residual_ln, rms_norm, pre_rms_norm).
 //
-// MI355X design: the backward kernels and the forward of narrow rows (< 1024) give ONE WAVE one row: it keeps the
-// row in NV*8 registers per lane (NV = compile-time vectors per lane), so the statistics need only a 64-lane
-// butterfly (no LDS, no __syncthreads) and the row is read from HBM exactly once; 256-thread blocks = 4 rows, every
-// access is 16 B/lane. The forward of wider rows gives a whole block one row (see norm_fwd_block_kernel).
+// MI355X design: rows narrower than 1024 give ONE WAVE one row: it keeps the row in NV*8 registers per lane (NV =
+// compile-time vectors per lane), so the statistics need only a 64-lane butterfly (no LDS, no __syncthreads) and the
+// row is read from HBM exactly once; 256-thread blocks = 4 rows, every access is 16 B/lane. Wider rows give a whole
+// block one row, forward (norm_fwd_block_kernel) and backward (norm_bwd_block_kernel).
 // Backward: pass 1 over the row accumulates the dot products and the per-lane dgamma/dbeta partials, pass 2
 // re-reads the (L1/L2-hot) row to write dx. dgamma/dbeta partials are reduced across the block's 4 waves in LDS
 // and written as one fp32 row per block, then summed by a column kernel (deterministic, no float atomics).
@@ -469,9 +469,118 @@ __global__ void __launch_bounds__(256) norm_fwd_block_kernel(const T* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------------ wide-row backward
+// Rows of 1024 - 8192 elements: a 256-thread block walks rows blockIdx.x, + gridDim.x, ...; thread t owns the columns
+// (k * 256 + t) * 8 .. + 7 of every row it sees, so its dgamma / dbeta sums stay in registers for the whole launch and
+// go straight to the partial buffer (no [4][H] LDS staging: at H = 8192 that staging is 128 KB, one block per CU, and
+// the wave-per-row kernels above fall to 1.8 - 3.9 TB/s). x, dy, dres and gamma stay packed in registers between the
+// reduction pass and the dx pass; the two row sums cross waves through 8 LDS words, double-buffered by row parity so a
+// row costs one barrier.
+template <typename T, int NB, bool ADD_DRES, bool LN>
+__global__ void __launch_bounds__(256) norm_bwd_block_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const T* __restrict__ gamma,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const T* __restrict__ dres, T* __restrict__ dx,
+                                                             float* __restrict__ part, int64_t rows, int H) {
+  __shared__ float red[2][2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float dg[NB][8], db[LN ? NB : 1][8];
+  typename Raw8<T>::type wraw[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    zero8(dg[k]);
+    if (LN) zero8(db[k < (LN ? NB : 1) ? k : 0]);
+    const int c = (k * 256 + tid) * 8;
+    if (c < H) wraw[k] = ld_raw8(gamma + c);
+  }
+  const float invH = 1.f / H;
+  int par = 0;
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x, par ^= 1) {
+    const float rs = rstd[row], mu = LN ? mean[row] : 0.f;
+    const T* xr = x + row * H;
+    const T* gr = dy + row * H;
+    typename Raw8<T>::type xraw[NB], graw[NB], draw[ADD_DRES ? NB : 1];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int c = (k * 256 + tid) * 8;
+      if (c < H) {
+        xraw[k] = ld_raw8(xr + c);
+        graw[k] = ld_raw8(gr + c);
+        if constexpr (ADD_DRES) draw[k] = ld_raw8(dres + row * H + c);
+      }
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      if ((k * 256 + tid) * 8 < H) {
+        float xv[8], gv[8], ww[8];
+        raw_to_f<T>(xraw[k], xv);
+        raw_to_f<T>(graw[k], gv);
+        raw_to_f<T>(wraw[k], ww);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - mu) * rs;
+          dg[k][j] = fmaf(gv[j], xh, dg[k][j]);
+          if (LN) db[k < (LN ? NB : 1) ? k : 0][j] += gv[j];
+          const float g = gv[j] * ww[j];
+          if (LN) s1 += g;
+          s2 = fmaf(g, xh, s2);
+        }
+      }
+    }
+    if (LN) s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      if (LN) red[par][0][wid] = s1;
+      red[par][1][wid] = s2;
+    }
+    __syncthreads();
+    const float m1 = LN ? (red[par][0][0] + red[par][0][1] + red[par][0][2] + red[par][0][3]) * invH : 0.f;
+    const float m2 = (red[par][1][0] + red[par][1][1] + red[par][1][2] + red[par][1][3]) * invH;
+    // opaque to the optimiser: the dx pass re-converts from the packed registers instead of keeping fp32 copies alive
+    launder_raw<T, NB>(xraw, graw);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int c = (k * 256 + tid) * 8;
+      if (c < H) {
+        float xv[8], gv[8], ww[8], o[8];
+        raw_to_f<T>(xraw[k], xv);
+        raw_to_f<T>(graw[k], gv);
+        raw_to_f<T>(wraw[k], ww);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (gv[j] * ww[j] - m1 - (xv[j] - mu) * rs * m2);
+        if constexpr (ADD_DRES) {
+          float d2[8];
+          raw_to_f<T>(draw[k], d2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += d2[j];
+        }
+        Vec8<T>::store(dx + row * H + c, o);
+      }
+    }
+  }
+  // this block's column sums: RMSNorm part[b][0:H]; LayerNorm dgamma part[b][0:H], dbeta part[b][H:2H]
+  const int64_t ld = LN ? 2 * (int64_t)H : H;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int c = (k * 256 + tid) * 8;
+    if (c < H) {
+      float* p = part + blockIdx.x * ld + c;
+      *reinterpret_cast<f32x4*>(p) = f32x4{dg[k][0], dg[k][1], dg[k][2], dg[k][3]};
+      *reinterpret_cast<f32x4*>(p + 4) = f32x4{dg[k][4], dg[k][5], dg[k][6], dg[k][7]};
+      if (LN) {
+        float (&b)[8] = db[k < (LN ? NB : 1) ? k : 0];
+        *reinterpret_cast<f32x4*>(p + H) = f32x4{b[0], b[1], b[2], b[3]};
+        *reinterpret_cast<f32x4*>(p + H + 4) = f32x4{b[4], b[5], b[6], b[7]};
+      }
+    }
+  }
+}
+
 }  // namespace
 
-#define DISPATCH_T(dt, ...)                                    \
+#define DISPATCH_T(dt, ...)                                   \
   do {                                                         \
     if ((dt) == DS_F32) { using T = float; __VA_ARGS__; }      \
     else if ((dt) == DS_BF16) { using T = bf16; __VA_ARGS__; } \
@@ -519,12 +628,39 @@ static void launch_block_norm(const void* x, const void* r, const void* g, const
 #undef DS_BLOCK_NORM
 }
 
+// Wide-row backward launch (H >= 1024): nb persistent blocks, NB = chunks per thread.
+template <typename T, bool LN>
+static void launch_block_norm_bwd(const void* dy, const void* x, const void* g, const float* mean, const float* rstd,
+                                  const void* dres, void* dx, float* part, int nb, int64_t rows, int H,
+                                  hipStream_t s) {
+  const int cb = (H + 2047) / 2048;
+#define DS_BLOCK_NORM_BWD(NB_)                                                                                     \
+  do {                                                                                                             \
+    if (dres)                                                                                                      \
+      hipLaunchKernelGGL((norm_bwd_block_kernel<T, NB_, true, LN>), dim3(nb), dim3(256), 0, s, (const T*)dy,       \
+                         (const T*)x, (const T*)g, mean, rstd, (const T*)dres, (T*)dx, part, rows, H);             \
+    else                                                                                                           \
+      hipLaunchKernelGGL((norm_bwd_block_kernel<T, NB_, false, LN>), dim3(nb), dim3(256), 0, s, (const T*)dy,      \
+                         (const T*)x, (const T*)g, mean, rstd, nullptr, (T*)dx, part, rows, H);                    \
+  } while (0)
+  if (cb <= 1) DS_BLOCK_NORM_BWD(1);
+  else if (cb <= 2) DS_BLOCK_NORM_BWD(2);
+  else DS_BLOCK_NORM_BWD(4);
+#undef DS_BLOCK_NORM_BWD
+}
+
+static bool bwd_wave_rows() {  // measurement switch: DS_NORM_BWD_WAVE=1 keeps the wave-per-row backward at every width
+  static const bool v = [] { const char* e = getenv("DS_NORM_BWD_WAVE"); return e && e[0] == '1'; }();
+  return v;
+}
+
 static constexpr int kMaxHidden = 8192;      // backward kernels
 static constexpr int kMaxHiddenFwd = 16384;  // forward kernels
 static int norm_grid(int64_t rows) { return ds_grid_for((rows + 3) / 4, 1, 256 * 8); }
 
 // Number of fp32 partial rows the backward writes for `rows`. The host allocates part[(nb + 32) * H] for RMSNorm
 // and part[(nb + 32) * 2H] for LayerNorm (the trailing 32 rows are the column-sum stage buffer).
+// (512 = two persistent blocks per CU: measured best for the wide-row backward against 256 / 768 / 1024 / 2048)
 extern "C" int ds_norm_bwd_blocks(int64_t rows) { return ds_grid_for((rows + 3) / 4, 1, 512); }
 
 extern "C" int ds_rms_fwd(const void* x, const void* r, const void* w, void* y, void* res_out, float* rstd,
@@ -555,6 +691,13 @@ extern "C" int ds_rms_bwd(const void* dy, const void* x, const void* w, const fl
   if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
   const int nb = ds_norm_bwd_blocks(rows);
+  if (block_rows(H) && !bwd_wave_rows()) {
+    DISPATCH_T(dtype, (launch_block_norm_bwd<T, false>(dy, x, w, nullptr, rstd, dres, dx, part, nb, rows, H, s)));
+    DS_CHECK_LAUNCH();
+    DISPATCH_T(dtype, colsum<T>(part, nb, H, H, part + (int64_t)nb * H, (T*)dw, s));
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t lds = 4 * (size_t)H * sizeof(float);
   DISPATCH_T(dtype, DISPATCH_NV(H, {
     if (dres)
@@ -599,8 +742,11 @@ extern "C" int ds_ln_bwd(const void* dy, const void* x, const void* g, const flo
   if (H % 8 != 0 || H > kMaxHidden) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
   const int nb = ds_norm_bwd_blocks(rows);
+  const bool blk = block_rows(H) && !bwd_wave_rows();
+  if (blk)
+    DISPATCH_T(dtype, (launch_block_norm_bwd<T, true>(dy, x, g, mean, rstd, dres, dx, part, nb, rows, H, s)));
   const size_t lds = 4 * (size_t)H * sizeof(float);
-  DISPATCH_T(dtype, DISPATCH_NV(H, {
+  if (!blk) DISPATCH_T(dtype, DISPATCH_NV(H, {
     if (dres)
       hipLaunchKernelGGL((ln_bwd_kernel<T, NV, true>), dim3(nb), dim3(256), lds, s, (const T*)dy, (const T*)x,
                          (const T*)g, mean, rstd, (const T*)dres, (T*)dx, part, rows, H);

@@ -130,7 +130,7 @@ def test_rms_norm_fwd_bwd(dtype, H, residual):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("H", [768, 1024, 4096])
+@pytest.mark.parametrize("H", [768, 1024, 4096, 5120, 8192])
 def test_layer_norm_fwd_bwd(dtype, H):
     from deepspeedsyclsupport_amd.ops.transformer import functional as DF
     torch.manual_seed(4)
@@ -148,6 +148,35 @@ def test_layer_norm_fwd_bwd(dtype, H):
     tol = dict(rtol=5e-2, atol=5e-1) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(g.grad.float(), gf.grad, **tol)
     torch.testing.assert_close(b.grad.float(), bf.grad, **tol)
+
+
+@pytest.mark.parametrize("H", [1032, 2048, 5120])
+@pytest.mark.parametrize("kind", ["rms", "ln"])
+def test_norm_backward_many_rows(kind, H):
+    """More rows than persistent blocks (every block walks several rows, the column partials of all blocks are
+    summed) and a width that is not a multiple of the block's 2048-element step."""
+    from deepspeedsyclsupport_amd.ops.transformer import functional as DF
+    torch.manual_seed(6)
+    rows = 2100
+    x = torch.randn(rows, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    g = (1 + 0.1 * torch.randn(H, device="cuda", dtype=torch.bfloat16)).requires_grad_(True)
+    b = (0.1 * torch.randn(H, device="cuda", dtype=torch.bfloat16)).requires_grad_(True)
+    xf, gf, bf = [t.detach().float().requires_grad_(True) for t in (x, g, b)]
+    if kind == "rms":
+        y = DF.rms_norm(x, g, 1e-5)
+        yr = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * gf
+    else:
+        y = DF.layer_norm(x, g, b, 1e-5)
+        yr = F.layer_norm(xf, (H, ), gf, bf, 1e-5)
+    gy = torch.randn_like(yr).bfloat16().float()
+    (y.float() * gy).sum().backward()
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xf.grad, **TOL[torch.bfloat16])
+    # column sums over 2100 rows of bf16-rounded products: compare against the fp32 sum with a relative bound
+    scale = float(gf.grad.abs().max())
+    assert float((g.grad.float() - gf.grad).abs().max()) <= 2e-2 * scale
+    if kind == "ln":
+        assert float((b.grad.float() - bf.grad).abs().max()) <= 2e-2 * float(bf.grad.abs().max())
 
 
 @pytest.mark.parametrize("act", ["silu", "gelu", "gelu_tanh", "relu"])
