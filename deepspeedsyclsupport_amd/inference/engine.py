@@ -70,6 +70,19 @@ class InferenceEngine(torch.nn.Module):
         self.injected = False
         self.encoder_injected = 0
         from ..module_inject import encoder as enc
+        if self.injection_dict:
+            # user-specified tensor parallelism (reference engine.py:135-154): only the listed blocks are sharded
+            if config.replace_with_kernel_inject:
+                raise ValueError("Cannot use both user specified injection policy and kernel injection")
+            from ..module_inject.auto_tp import AutoTP
+            AutoTP(model, self.mp_group, self.tp_size, self.tp_rank, injection_policy=self.injection_dict).apply()
+            self.module = model.to(self.device)
+            if self.dtype in (torch.float16, torch.bfloat16, torch.float32):
+                self.module = self.module.to(self.dtype)
+            self.module.eval()
+            log_dist(f"InferenceEngine: user injection policy over {len(self.injection_dict)} block classes, "
+                     f"tp={self.tp_size}", ranks=[0])
+            return
         if not isinstance(model, torch.nn.Module):
             # diffusers-style pipeline (reference engine.py: generic_injection for non-Module models)
             from ..module_inject.replace_module import generic_injection

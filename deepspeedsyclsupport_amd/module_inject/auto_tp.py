@@ -42,7 +42,12 @@ def _slice_rows(w, r, tp):
 
 class AutoTP:
 
-    def __init__(self, model, mp_group, tp_size, tp_rank, kv_heads=None):
+    def __init__(self, model, mp_group, tp_size, tp_rank, kv_heads=None, injection_policy=None):
+        """`injection_policy`: {block class: name or tuple of names of the linears whose output is all-reduced}
+        (reference `inference/engine.py:135-154`, `module_inject/replace_module.py:266-300`): inside every instance
+        of a listed class the named linears are split along their input features and all-reduced, every other
+        linear of the block along its output features; nothing outside those blocks is touched."""
+        self.policy = self._normalise_policy(injection_policy)
         self.model = model
         self.mp_group = mp_group
         self.tp = tp_size
@@ -97,16 +102,90 @@ class AutoTP:
         return LinearAllreduce(nn.Parameter(w, requires_grad=False),
                                None if b is None else nn.Parameter(b.clone(), requires_grad=False), self.mp_group)
 
+    # ------------------------------------------------------------------------------------------ user policy
+    @staticmethod
+    def _normalise_policy(policy):
+        if not policy:
+            return None
+        out = {}
+        for cls, names in policy.items():
+            if not (isinstance(cls, type) and issubclass(cls, nn.Module)):
+                raise TypeError(f"{cls} is not a subclass of torch.nn.Module")
+            out[cls] = (names, ) if isinstance(names, str) else tuple(names)
+        return out
+
+    @staticmethod
+    def _ends_with(name, suffix):
+        return ("." + name).endswith("." + suffix.lstrip("."))
+
+    def _policy_targets(self):
+        """(qualified name, module, is_row_parallel) of every linear inside a block the user policy lists."""
+        all_names = [n for n, _ in self.model.named_modules()]
+        for names in self.policy.values():
+            for suffix in names:
+                if not any(self._ends_with(n, suffix) for n in all_names):
+                    raise ValueError(f"Injection policy layer '{suffix}' not valid.")
+        seen, out = set(), []
+        for bname, blk in self.model.named_modules():
+            rows = next((v for k, v in self.policy.items() if isinstance(blk, k)), None)
+            if rows is None:
+                continue
+            for rel, m in blk.named_modules():
+                if not rel or not (isinstance(m, nn.Linear) or _is_conv1d(m)):
+                    continue
+                full = f"{bname}.{rel}" if bname else rel
+                if full in seen:
+                    continue
+                seen.add(full)
+                out.append((full, m, any(self._ends_with(rel, s) for s in rows)))
+        return out
+
+    @staticmethod
+    def tp_parser(model):
+        """[(block class, tuple of all-reduce linear names)] derived from the model's structure (reference
+        `module_inject/auto_tp.py:271-311`): the repeated blocks are the children of ModuleLists; inside a block a
+        linear is all-reduced when its name is a known output projection, when it is the last linear before a
+        normalisation layer, or when it is the last linear of the block."""
+        found = {}
+        for _, lst in model.named_modules():
+            if not isinstance(lst, nn.ModuleList) or len(lst) == 0:
+                continue
+            blk = lst[0]
+            if sum(1 for _ in blk.modules()) < 3 or type(blk) in found:
+                continue
+            rows, last_linear = [], None
+            for rel, m in blk.named_modules():
+                if not rel:
+                    continue
+                if isinstance(m, nn.Linear) or _is_conv1d(m):
+                    last_linear = rel
+                    if AutoTP.is_row_parallel(rel):
+                        rows.append(rel)
+                elif "norm" in type(m).__name__.lower() or rel.split(".")[-1] in ("ln", "LayerNorm", "layer_norm"):
+                    if last_linear is not None and last_linear not in rows:
+                        rows.append(last_linear)
+                    last_linear = None
+            if last_linear is not None and last_linear not in rows:  # the block's output projection
+                rows.append(last_linear)
+            if rows:
+                found[type(blk)] = tuple(dict.fromkeys(rows))
+        if not found:
+            raise ValueError("Not able to determine model policy automatically. Please provide policy.")
+        return list(found.items())
+
     # ------------------------------------------------------------------------------------------ apply
     def apply(self):
         if self.tp <= 1:
             return self.model
-        targets = []
-        for name, m in self.model.named_modules():
-            if (isinstance(m, nn.Linear) or _is_conv1d(m)) and self.in_block(name):
-                targets.append((name, m))
-        for name, m in targets:
-            new = self._row(name, m) if self.is_row_parallel(name) else self._column(name, m)
+        if self.policy is not None:
+            targets = self._policy_targets()
+        else:
+            targets = []
+            for name, m in self.model.named_modules():
+                if (isinstance(m, nn.Linear) or _is_conv1d(m)) and self.in_block(name):
+                    targets.append((name, m, self.is_row_parallel(name)))
+        for name, m, row in targets:
+            new = self._row(name, m) if row else self._column(name, m)
             parent_name, _, leaf = name.rpartition(".")
             parent = self.model.get_submodule(parent_name) if parent_name else self.model
             setattr(parent, leaf, new)
@@ -115,8 +194,13 @@ class AutoTP:
         return self.model
 
     def _fix_attrs(self):
+        in_policy = set()
+        if self.policy is not None:  # the listed blocks (and what they contain) hold the head counts
+            for _, blk in self.model.named_modules():
+                if isinstance(blk, tuple(self.policy)):
+                    in_policy.update(id(m) for m in blk.modules())
         for name, m in self.model.named_modules():
-            if not re.search(r"attn|attention", name.split(".")[-1] if name else "", re.I):
+            if id(m) not in in_policy and not re.search(r"attn|attention", name.split(".")[-1] if name else "", re.I):
                 continue
             for a in HEAD_ATTRS:
                 v = getattr(m, a, None)

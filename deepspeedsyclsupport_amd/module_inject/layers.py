@@ -19,6 +19,10 @@ class LinearAllreduce(nn.Module):
                                                                                              requires_grad=False)
         self.mp_group = mp_group
 
+    # local shapes, as the nn.Linear this stands in for would report them
+    in_features = property(lambda self: self.weight.shape[1])
+    out_features = property(lambda self: self.weight.shape[0])
+
     def forward(self, input):
         out = F.linear(input, self.weight)
         if self.mp_group is not None and dist.get_world_size(self.mp_group) > 1:
@@ -56,6 +60,9 @@ class LinearLayer(nn.Module):
         self.weight = weight if isinstance(weight, nn.Parameter) else nn.Parameter(weight, requires_grad=False)
         self.bias = bias if (bias is None or isinstance(bias, nn.Parameter)) else nn.Parameter(bias,
                                                                                              requires_grad=False)
+
+    in_features = property(lambda self: self.weight.shape[1])
+    out_features = property(lambda self: self.weight.shape[0])
 
     def forward(self, input):
         return F.linear(input, self.weight, self.bias)
