@@ -14,9 +14,9 @@ from typing import Iterable, Tuple
 
 import torch
 
-from ..model_implementations.transformer import DSInferenceModel, RaggedMeta
+from ..model_implementations.transformer import DSInferenceModel
 from .config_v2 import AllocationMode, RaggedInferenceEngineConfig
-from .ragged import DSStateManager, PlaceholderSequenceDescriptor
+from .ragged import DSStateManager, PlaceholderSequenceDescriptor, RaggedBatchWrapper
 from .scheduling_utils import SchedulingError, SchedulingResult
 
 
@@ -42,6 +42,7 @@ class InferenceEngineV2:
         model.allocate_cache(num_blocks, bs)
         self._state_manager = DSStateManager(sm, num_blocks, bs)
         self._device = model.device if model.device is not None else torch.device("cpu")
+        self._batch = RaggedBatchWrapper(sm, bs, self._device)
 
     # ------------------------------------------------------------------------------------------ properties
     @property
@@ -65,24 +66,18 @@ class InferenceEngineV2:
             res = self.can_schedule(uids, [t.numel() for t in toks])
             if res != SchedulingResult.Success:
                 raise SchedulingError(res)
+        batch = self._batch
+        batch.clear()
         seqs = []
         for uid, t in zip(uids, toks):
             seq = self._state_manager.get_or_create_sequence(uid)
             self._state_manager.allocate_blocks(seq, t.numel())
             seq.pre_forward(t.numel())
+            batch.insert_sequence(seq, t, do_checks=False)
             seqs.append(seq)
-        # decode sequences first (the paged decode kernel takes a leading slice), then prompts / chunks
-        order = sorted(range(len(uids)), key=lambda i: 0 if (toks[i].numel() == 1 and seqs[i].seen_tokens > 0) else 1)
-        n_decode = sum(1 for i in order if toks[i].numel() == 1 and seqs[i].seen_tokens > 0)
-        oseqs = [seqs[i] for i in order]
-        meta = RaggedMeta.build([s.seen_tokens for s in oseqs], [toks[i].numel() for i in order],
-                                [s.blocks for s in oseqs], n_decode, self._state_manager.block_size, self._device)
-        ids = torch.cat([toks[i] for i in order]).to(self._device, non_blocking=True)
-        logits = self._model.forward_ragged(ids, meta)
-        inv = [0] * len(order)
-        for j, i in enumerate(order):
-            inv[i] = j
-        out = logits.index_select(0, torch.tensor(inv, device=logits.device))
+        batch.finalize()
+        logits = self._model.forward_ragged(batch.input_ids(), batch.meta)
+        out = batch.restore_order(logits)
         for s in seqs:
             s.post_forward()
         return out

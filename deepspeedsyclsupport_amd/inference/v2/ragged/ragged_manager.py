@@ -1,39 +1,8 @@
-"""Sequence / KV-block bookkeeping for the ragged engine (reference `inference/v2/ragged/{ragged_manager.py:19,
-sequence_descriptor.py, blocked_allocator.py}`)."""
+"""Sequence tracking and KV-block allocation (reference `inference/v2/ragged/ragged_manager.py:19`)."""
 import torch
 
-from ..kv_cache import BlockedAllocator
-
-
-class DSSequenceDescriptor:
-
-    def __init__(self, uid, block_size):
-        self.uid = uid
-        self.seen_tokens = 0
-        self.in_flight_tokens = 0
-        self.blocks = []
-        self.block_size = block_size
-
-    @property
-    def cur_allocated_blocks(self):
-        return len(self.blocks)
-
-    def blocks_needed(self, new_tokens):
-        total = self.seen_tokens + new_tokens
-        return max(0, -(-total // self.block_size) - len(self.blocks))
-
-    def pre_forward(self, n):
-        self.in_flight_tokens = n
-
-    def post_forward(self):
-        self.seen_tokens += self.in_flight_tokens
-        self.in_flight_tokens = 0
-
-
-class PlaceholderSequenceDescriptor(DSSequenceDescriptor):
-
-    def __init__(self, block_size=64):
-        super().__init__(-1, block_size)
+from ...kv_cache import BlockedAllocator
+from .sequence_descriptor import DSSequenceDescriptor
 
 
 class DSStateManager:
@@ -47,6 +16,10 @@ class DSStateManager:
     @property
     def n_tracked_sequences(self):
         return len(self._seqs)
+
+    @property
+    def tracked_sequences(self):
+        return self._seqs
 
     @property
     def free_blocks(self):
@@ -66,7 +39,7 @@ class DSStateManager:
     def allocate_blocks(self, seq, n_tokens):
         need = seq.blocks_needed(n_tokens)
         if need:
-            seq.blocks.extend(self.allocator.allocate(need))
+            seq.extend_kv_cache(self.allocator.allocate(need))
 
     def flush_sequence(self, uid):
         seq = self._seqs.pop(uid, None)

@@ -20,6 +20,16 @@ def _create_logger(name="DeepSpeedAMD", level=logging.INFO):
     return lg
 
 
+class LoggerFactory:
+    """Named loggers with the package's format (reference `utils/logging.py:LoggerFactory`)."""
+
+    @staticmethod
+    def create_logger(name=None, level=logging.INFO):
+        if name is None:
+            raise ValueError("name for logger cannot be None")
+        return _create_logger(name, level)
+
+
 logger = _create_logger(level=getattr(logging, os.environ.get("DS_LOG_LEVEL", "INFO").upper(), logging.INFO))
 
 
