@@ -120,9 +120,7 @@ class _RotaryAppendBase(DSKernelBase):
                 DF.apply_rotary_pos_emb(k, cos, sin, position_ids=pos, rotary_dim=rot, interleaved=interleaved)
             T._kv_append_ragged(k[0], v[0], kc, vc, meta)
             q = q[0]
-        # q goes back into the leading columns of qkv, as the reference rotates in place
-        qkv[:, :self.hq * D].copy_(q.reshape(Tn, self.hq * D))
-        return qkv[:, :self.hq * D]
+        return q.reshape(Tn, self.hq * D)   # rotated queries (qkv itself is left as it was)
 
 
 class BlockedRotaryEmbeddings(_RotaryAppendBase):
