@@ -558,28 +558,32 @@ def shard_layer(spec, lw, r, tp):
     return out
 
 
-def load_into(model: DSInferenceModel, top, layers):
-    spec, r, tp = model.spec, model.tp_rank, model.tp_size
+def _put(param, src):
+    if param is None or src is None:
+        return
+    param.data.copy_(src.detach().to(param.dtype))
 
-    def put(param, src):
-        if param is None or src is None:
-            return
-        param.data.copy_(src.detach().to(param.dtype))
 
-    for layer, lw in zip(model.layers, layers):
-        for name, t in shard_layer(spec, lw, r, tp).items():
-            put(getattr(layer, name), t)
-    put(model.embed, top["embed"])
+def load_layer(model: DSInferenceModel, idx, lw):
+    """Canonical full weights of layer `idx` -> this rank's shard of the injected layer."""
+    for name, t in shard_layer(model.spec, lw, model.tp_rank, model.tp_size).items():
+        _put(getattr(model.layers[idx], name), t)
+
+
+def load_top(model: DSInferenceModel, top):
+    """Embeddings, final norm and LM head (vocab rows sharded over the ranks, zero-padded)."""
+    spec, r = model.spec, model.tp_rank
+    _put(model.embed, top["embed"])
     if model.pos_embed is not None:
         pe = top["pos_embed"]
         model.pos_embed.data.zero_()
         n = min(pe.shape[0], model.pos_embed.shape[0])
         model.pos_embed.data[:n].copy_(pe[:n].to(model.dtype))
     if spec.embed_norm:
-        put(model.embed_ln_w, top["embed_ln_w"])
-        put(model.embed_ln_b, top["embed_ln_b"])
-    put(model.norm_w, top["norm_w"])
-    put(model.norm_b, top.get("norm_b"))
+        _put(model.embed_ln_w, top["embed_ln_w"])
+        _put(model.embed_ln_b, top["embed_ln_b"])
+    _put(model.norm_w, top["norm_w"])
+    _put(model.norm_b, top.get("norm_b"))
     V, vl = spec.vocab_size, model.vocab_local
     lm = top["lm_head"]
     model.lm_head.data.zero_()
@@ -589,6 +593,21 @@ def load_into(model: DSInferenceModel, top, layers):
         if model.lm_head_b is not None and top.get("lm_head_b") is not None:
             model.lm_head_b.data.zero_()
             model.lm_head_b.data[:hi - lo].copy_(top["lm_head_b"][lo:hi].to(model.dtype))
+
+
+def load_into(model: DSInferenceModel, top, layers):
+    for i, lw in enumerate(layers[:len(model.layers)]):
+        load_layer(model, i, lw)
+    load_top(model, top)
+
+
+def spec_from_config(hf_config):
+    """The `DSModelSpec` of a HF config alone: the architecture is instantiated on the meta device (no weight
+    memory) and read by its converter."""
+    import transformers
+    with torch.device("meta"):
+        skeleton = transformers.AutoModelForCausalLM.from_config(hf_config)
+    return extract(skeleton)[0]
 
 
 def from_model(model, tp_group=None, tp_size=1, tp_rank=0, dtype=torch.bfloat16, device=None, max_positions=None):

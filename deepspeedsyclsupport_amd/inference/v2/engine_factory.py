@@ -13,6 +13,16 @@ def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = 
     already-instantiated HF / native model."""
     engine_config = engine_config or RaggedInferenceEngineConfig()
     if isinstance(path_or_model, str):
+        import os
+        if os.path.exists(os.path.join(path_or_model, "ds_model_config.json")):
+            return build_engine_from_ds_checkpoint(path_or_model, engine_config, debug_level, device)
+        from .checkpoint import HuggingFaceCheckpointEngine
+        from .model_implementations import POLICIES
+        ckpt = HuggingFaceCheckpointEngine(path_or_model)
+        policy_cls = POLICIES.get(ckpt.model_config.model_type)
+        if policy_cls is not None:
+            # streamed load: checkpoint tensors go layer by layer into the sharded device model
+            return _engine_from_policy(policy_cls(ckpt.model_config, checkpoint_engine=ckpt), engine_config, dtype)
         import transformers
         model = transformers.AutoModelForCausalLM.from_pretrained(path_or_model, torch_dtype=torch.float32,
                                                                   local_files_only=True)
@@ -41,6 +51,33 @@ def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = 
         ds_model.quantize_weights(8 if q == "int8" else 4)
     else:
         _apply_decode_layout(ds_model, engine_config.decode_layout, tp, device)
+    return InferenceEngineV2(ds_model, engine_config)
+
+
+def _tp_group(tp):
+    """The tensor-parallel group of this rank (consecutive ranks), created on first use."""
+    from ... import comm as dist
+    from ..engine import InferenceEngine
+    group = InferenceEngine.inference_mp_group
+    if group is None:
+        world, me = dist.get_world_size(), dist.get_rank()
+        for s in range(0, world, tp):
+            g = dist.new_group(list(range(s, s + tp)))
+            if s <= me < s + tp:
+                group = g
+    return group
+
+
+def _engine_from_policy(policy, engine_config, dtype=torch.bfloat16):
+    """Policy (checkpoint engine + containers) -> model -> engine (reference `engine_factory.py:65-129`)."""
+    tp = engine_config.tensor_parallel.tp_size
+    policy.dtype = dtype
+    ds_model = policy.build_model(engine_config, _tp_group(tp) if tp > 1 else None)
+    q = engine_config.quantization.quantization_mode
+    if q in ("int8", "int4"):
+        ds_model.quantize_weights(8 if q == "int8" else 4)
+    else:
+        _apply_decode_layout(ds_model, engine_config.decode_layout, tp, torch.device(ds_model.device))
     return InferenceEngineV2(ds_model, engine_config)
 
 
