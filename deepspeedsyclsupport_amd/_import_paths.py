@@ -42,7 +42,153 @@ PATHS = {
     "constants": [("comm.comm", {"TORCH_DISTRIBUTED_DEFAULT_PORT": "TORCH_DISTRIBUTED_DEFAULT_PORT",
                                  "default_pg_timeout": "default_pg_timeout"})],
     "pydantic_v1": [("runtime.config_utils", "*")],
+    # ---- training runtime
+    "runtime.activation_checkpointing.config": [("runtime.config", {"DeepSpeedActivationCheckpointingConfig":
+                                                                    "ActivationCheckpointingConfig"})],
+    "runtime.checkpoint_engine.torch_checkpoint_engine": [("runtime.checkpoint_engine.checkpoint_engine",
+                                                           {"TorchCheckpointEngine": "TorchCheckpointEngine"})],
+    "runtime.checkpoint_engine.nebula_checkpoint_engine": [("runtime.checkpoint_engine.checkpoint_engine",
+                                                            {"NebulaCheckpointEngine": "AsyncCheckpointEngine"})],
+    "runtime.comm.nccl": [("runtime.comm.compressed", {"NcclBackend": "CompressedBackend"})],
+    "runtime.comm.mpi": [("runtime.comm.compressed", {"MpiBackend": "CompressedBackend"})],
+    "runtime.comm.hccl": [("runtime.comm.compressed", {"HcclBackend": "CompressedBackend"})],
+    "runtime.compression.cupy": [("runtime.comm.compressed", {"pack_signs": "pack_signs",
+                                                              "unpack_signs": "unpack_signs"})],
+    "runtime.swap_tensor.async_swapper": [("runtime.swap_tensor.tensor_swapper",
+                                           {"AsyncTensorSwapper": "AsyncTensorSwapper"})],
+    "runtime.swap_tensor.partitioned_optimizer_swapper": [("runtime.swap_tensor.optimizer_swapper",
+                                                           {"PartitionedOptimizerSwapper": "OptimizerStateSwapper"})],
+    "runtime.swap_tensor.pipelined_optimizer_swapper": [("runtime.swap_tensor.optimizer_swapper",
+                                                         {"PipelinedOptimizerSwapper": "OptimizerStateSwapper"})],
+    "runtime.swap_tensor.optimizer_utils": [("runtime.swap_tensor.optimizer_swapper",
+                                             {"OptimizerSwapper": "OptimizerStateSwapper", "NvmeFlat": "NvmeFlat"})],
+    "runtime.swap_tensor.partitioned_param_swapper": [("runtime.swap_tensor.param_store",
+                                                       {"AsyncPartitionedParameterSwapper": "ParamNvmeStore"})],
+    "runtime.swap_tensor.aio_config": [("runtime.config", {"AIOConfig": "AIOConfig"})],
+    "runtime.data_pipeline.config": [("runtime.config", {"DeepSpeedConfig": "DeepSpeedConfig"})],
+    "runtime.data_pipeline.data_routing.helper": [("runtime.data_pipeline.data_routing.basic_layer",
+                                                   {"convert_to_random_ltd": "convert_to_random_ltd"})],
+    "runtime.data_pipeline.data_routing.utils": [("ops.random_ltd", "*")],
+    "runtime.data_pipeline.data_sampling.utils": [("runtime.data_pipeline.data_sampling.indexed_dataset", "*"),
+                                                  ("runtime.data_pipeline.data_sampling.data_analyzer",
+                                                   {"split_index": "split_index", "split_dataset": "split_dataset"})],
+    "runtime.zero.mics_utils": [("runtime.zero", "*")],
+    "autotuning.scheduler": [("autotuning.autotuner", {"ResourceManager": "ResourceManager"})],
+    "monitor.utils": [("monitor.monitor", {"check_tb_availability": "check_tb_availability",
+                                           "check_wandb_availability": "check_wandb_availability"})],
+    # ---- ops
+    "ops.deepspeed4science.evoformer_attn": [("ops.deepspeed4science", "*")],
+    "ops.random_ltd.dropping_utils": [("ops.random_ltd", "*")],
+    "ops.sparse_attention.bert_sparse_self_attention": [("ops.sparse_attention.sparse_self_attention",
+                                                         {"BertSparseSelfAttention": "BertSparseSelfAttention"})],
+    "ops.sparse_attention.sparse_attention_utils": [("ops.sparse_attention.sparse_self_attention",
+                                                     {"SparseAttentionUtils": "SparseAttentionUtils"})],
+    "ops.transformer.inference.bias_add": [("ops.spatial", {"nhwc_bias_add": "nhwc_bias_add"})],
+    "ops.transformer.inference.moe_inference": [
+        ("ops.transformer.inference.layer", {"DeepSpeedMoEInference": "DeepSpeedMoEInference"}),
+        ("ops.transformer.inference.config", {"DeepSpeedMoEInferenceConfig": "DeepSpeedMoEInferenceConfig"})],
+    "ops.transformer.inference.diffusers_attention": [("module_inject.diffusers",
+                                                       {"DeepSpeedDiffusersAttention": "DSDiffusersAttention"})],
+    "ops.transformer.inference.diffusers_transformer_block": [
+        ("module_inject.diffusers", {"DeepSpeedDiffusersTransformerBlock": "DSDiffusersTransformerBlock"})],
+    # ---- inference v1 model wrappers: one fused layer serves every architecture
+    "model_implementations.diffusers.unet": [("module_inject.diffusers", {"DSUNet": "DSUNet"})],
+    "model_implementations.diffusers.vae": [("module_inject.diffusers", {"DSVAE": "DSVAE"})],
+    "model_implementations.transformers.clip_encoder": [("module_inject.diffusers",
+                                                         {"DSClipEncoder": "DSClipEncoder"})],
+    "model_implementations.features.cuda_graph": [("module_inject.diffusers", {"CUDAGraph": "GraphedCall"})],
+    "model_implementations.transformers.ds_transformer": [
+        ("ops.transformer.inference.layer", {"DeepSpeedTransformerInference": "DeepSpeedTransformerInference"})],
+    "model_implementations.transformers.ds_base": [
+        ("ops.transformer.inference.layer", {"DeepSpeedTransformerBase": "DeepSpeedTransformerInference"})],
+    "model_implementations.transformers.ds_bert": [
+        ("ops.transformer.inference.layer", {"DeepSpeedBERTInference": "DeepSpeedTransformerInference"})],
+    "model_implementations.transformers.ds_bloom": [
+        ("ops.transformer.inference.layer", {"DeepSpeedBloomInference": "DeepSpeedTransformerInference"})],
+    "model_implementations.transformers.ds_gpt": [
+        ("ops.transformer.inference.layer", {"DeepSpeedGPTInference": "DeepSpeedTransformerInference"})],
+    "model_implementations.transformers.ds_llama2": [
+        ("ops.transformer.inference.layer", {"DeepSpeedLlama2Inference": "DeepSpeedTransformerInference"})],
+    "model_implementations.transformers.ds_megatron_gpt": [
+        ("ops.transformer.inference.layer", {"DeepSpeedMegatronGPTInference": "DeepSpeedTransformerInference"})],
+    "model_implementations.transformers.ds_opt": [
+        ("ops.transformer.inference.layer", {"DeepSpeedOPTInference": "DeepSpeedTransformerInference"})],
+    # ---- inference v2: the reference's one-class-per-file tree over this package's per-family modules
+    "inference.v2.ragged.blocked_allocator": [("inference.kv_cache", {"BlockedAllocator": "BlockedAllocator"})],
+    "inference.v2.ragged.kv_cache": [("inference.kv_cache", {"BlockedKVCache": "BlockedKVCache"})],
+    "inference.v2.ragged.manager_configs": [("inference.v2.config_v2", "*")],
+    **{f"inference.v2.kernels.core_ops.{d}.{f}": [("inference.v2.kernels.core_ops", {n: n for n in names})]
+       for d, f, names in (
+           ("bias_activations", "bias_activation", ("CUDABiasActivation", )),
+           ("blas_kernels", "blas_linear", ("BlasLibLinear", )),
+           ("cuda_layer_norm", "cuda_fp_ln_base", ("CUDAFPLNBase", )),
+           ("cuda_layer_norm", "cuda_ln", ("CUDAFPLN", )),
+           ("cuda_layer_norm", "cuda_post_ln", ("CUDAFPPostLN", )),
+           ("cuda_layer_norm", "cuda_pre_ln", ("CUDAFPPreLN", )),
+           ("cuda_rms_norm", "rms_norm_base", ("CUDARMSNormBase", )),
+           ("cuda_rms_norm", "rms_norm", ("CUDARMSNorm", )),
+           ("cuda_rms_norm", "rms_pre_norm", ("CUDARMSPreNorm", )),
+           ("gated_activations", "gated_activation", ("CUDAGatedActivation", )))},
+    **{f"inference.v2.kernels.cutlass_ops.{d}.{f}": [("inference.v2.kernels.cutlass_ops", {n: n})]
+       for d, f, n in (("mixed_gemm", "mixed_gemm", "MixedGEMM"), ("moe_gemm", "moe_gemm", "MoEGEMM"),
+                       ("moe_gemm", "mixed_moe_gemm", "MixedMoEGEMM"))},
+    **{f"inference.v2.kernels.ragged_ops.{d}.{f}": [("inference.v2.kernels.ragged_ops", {n: n for n in names})]
+       for d, f, names in (
+           ("atom_builder", "atom_builder", ("AtomBuilder", )),
+           ("blocked_flash", "blocked_flash", ("BlockedFlashAttn", "get_q_block_size", "get_kv_block_size")),
+           ("embed", "embed", ("RaggedEmbeddingKernel", )),
+           ("linear_blocked_kv_rotary", "blocked_kv_rotary", ("BlockedRotaryEmbeddings", )),
+           ("linear_blocked_kv_rotary", "blocked_trained_kv_rotary", ("BlockedTrainedRotaryEmbeddings", )),
+           ("linear_blocked_kv_rotary", "linear_blocked_kv_copy", ("LinearBlockedKVCopy", )),
+           ("logits_gather", "logits_gather", ("RaggedLogitsGather", )),
+           ("moe_gather", "moe_gather", ("MoEGather", )),
+           ("moe_scatter", "moe_scatter", ("MoEScatter", )),
+           ("top_k_gating", "top_k_gating", ("RaggedTopKGating", )))},
+    **{f"inference.v2.modules.configs.{f}": [("inference.v2.modules.configs", "*")]
+       for f in ("attention_configs", "embedding_config", "linear_config", "moe_config", "norm_config",
+                 "unembed_config")},
+    **{f"inference.v2.modules.interfaces.{f}": [("inference.v2.modules.interfaces", "*")]
+       for f in ("attention_base", "embedding_base", "linear_base", "moe_base", "post_norm_base", "pre_norm_base",
+                 "unembed_base")},
+    **{f"inference.v2.modules.implementations.{d}.{f}": [("inference.v2.modules.implementations", {n: n})]
+       for d, f, n in (("attention", "dense_blocked_attention", "DSDenseBlockedAttention"),
+                       ("embedding", "ragged_embedding", "DSRaggedEmbedding"),
+                       ("linear", "blas_fp_linear", "BlasFPLinear"),
+                       ("moe", "cutlass_multi_gemm", "DSMultiGemmMoE"),
+                       ("post_norm", "cuda_post_ln", "DSPostLNCUDAModule"),
+                       ("pre_norm", "cuda_pre_ln", "DSPreLNCUDAModule"),
+                       ("pre_norm", "cuda_pre_rms", "DSPreRMSCUDAModule"),
+                       ("unembed", "ragged_unembed", "DSRaggedUnembed"))},
+    **{f"inference.v2.model_implementations.common_parameters.{f}": [
+        ("inference.v2.model_implementations.common_parameters", "*")]
+       for f in ("attn_output_parameters", "embedding_parameters", "invfreq_parameters", "mlp_parameters",
+                 "moe_parameters", "norm_parameters", "qkv_parameters", "unembed_parameters")},
+    **{f"inference.v2.model_implementations.sharding.{f}": [("inference.v2.model_implementations.sharding", "*")]
+       for f in ("attn", "attn_out", "embedding", "mlp", "qkv", "types", "unembed", "utils")},
+    **{f"inference.v2.model_implementations.{a}.{f}": [("inference.v2.model_implementations.archs", "*")]
+       for a in ("llama_v2", "mistral", "mixtral", "opt", "phi", "falcon")
+       for f in ("container", "containers", "model", "policy")},
 }
+# (File modules of this package that sub-paths hang under — `core_ops.py`, `ragged_ops.py`, `configs.py`, ... — carry
+# `__path__ = []`, so the import system asks the finder for their "submodules".)
+
+
+
+_VIRTUAL = None
+
+
+def _virtual_packages():
+    """Proper prefixes of the served paths that are not served paths themselves."""
+    global _VIRTUAL
+    if _VIRTUAL is None:
+        _VIRTUAL = set()
+        for key in PATHS:
+            parts = key.split(".")
+            for i in range(1, len(parts)):
+                prefix = ".".join(parts[:i])
+                if prefix not in PATHS:
+                    _VIRTUAL.add(prefix)
+    return _VIRTUAL
 
 
 class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
@@ -50,8 +196,11 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
     def find_spec(self, fullname, path=None, target=None):
         if not fullname.startswith(_PKG + "."):
             return None
-        if fullname[len(_PKG) + 1:] in PATHS:
+        rel = fullname[len(_PKG) + 1:]
+        if rel in PATHS:
             return importlib.machinery.ModuleSpec(fullname, self)
+        if rel in _virtual_packages():
+            return importlib.machinery.ModuleSpec(fullname, self, is_package=True)
         return None
 
     def create_module(self, spec):
@@ -59,6 +208,10 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
 
     def exec_module(self, module):
         rel = module.__name__[len(_PKG) + 1:]
+        if rel not in PATHS:     # a directory of the reference's tree that only holds served paths
+            module.__path__ = []
+            module.__doc__ = f"Reference package `deepspeed.{rel}` (paths below it: `{_PKG}/_import_paths.py`)."
+            return
         module.__doc__ = f"Reference import path `deepspeed.{rel}` (see `{_PKG}/_import_paths.py`)."
         for real, names in PATHS[rel]:
             src = importlib.import_module(f"{_PKG}.{real}")

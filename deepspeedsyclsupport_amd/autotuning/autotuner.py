@@ -90,6 +90,8 @@ class Autotuner:
                 base_config = json.load(f)
         self.base = base_config
         at = base_config.get("autotuning", {})
+        from .config import DeepSpeedAutotuningConfig
+        DeepSpeedAutotuningConfig(**at)  # unknown keys / wrong types fail here, before any experiment is launched
         self.at = at
         self.results_dir = at.get("results_dir", "autotuning_results")
         self.exps_dir = at.get("exps_dir", "autotuning_exps")

@@ -17,6 +17,8 @@ from ....ops.transformer import functional as DF
 from ..inference_utils import ActivationType, DtypeEnum, act_name, elem_size
 from .ds_kernel import DSKernelBase
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 
 def _dtype(dt):
     return dt.value if isinstance(dt, DtypeEnum) else DtypeEnum(dt).value

@@ -3,4 +3,6 @@ moe_gemm}`): the implementations live in `ops/cutlass_ops.py` on the gfx950 int8
 GEMM."""
 from ....ops.cutlass_ops import MixedGEMM, MixedMoEGEMM, MoEGEMM
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 __all__ = ["MixedGEMM", "MoEGEMM", "MixedMoEGEMM"]

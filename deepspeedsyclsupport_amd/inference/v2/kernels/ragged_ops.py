@@ -29,6 +29,8 @@ from ..inference_utils import DtypeEnum
 from .core_ops import _check_dtype
 from .ds_kernel import DSKernelBase
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 HEAD_SIZES = tuple(T.PAGED_HEAD_DIMS)
 
 

@@ -4,6 +4,8 @@ import torch
 
 from .parameter_base import ParameterBase, ParamList, single
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 EmbeddingParameter = single("embed", "Word embedding table [vocab, hidden].")
 UnembedParameter = single("lm_head", "LM head [vocab, hidden].")
 InvFreqParameter = single("inv_freq", "Rotary inverse frequencies stored in the checkpoint (recomputed here).")

@@ -15,6 +15,8 @@ from typing import Optional, Tuple
 
 import torch
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 DEFAULT_SHARD_GRANULARITY = 32
 
 

@@ -6,6 +6,8 @@ from ..inference_utils import ActivationType, DtypeEnum, NormTypeEnum
 from ....runtime.config_utils import DeepSpeedConfigModel
 from .ds_module import DSModuleConfig
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 
 class PositionalEmbeddingType(Enum):
     none = "none"

@@ -22,6 +22,8 @@ from .interfaces import (DSEmbeddingBase, DSEmbeddingRegistry, DSLinearBase, DSL
                          DSMoERegistry, DSPostNormBase, DSPostNormRegistry, DSPreNormBase, DSPreNormRegistry,
                          DSSelfAttentionBase, DSSelfAttentionRegistry, DSUnembedBase, DSUnembedRegistry)
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 _FP = (torch.float16, torch.bfloat16, torch.float32)
 
 

@@ -10,6 +10,8 @@ from .configs import (DSEmbeddingsConfig, DSLinearConfig, DSMoEConfig, DSNormCon
 from .ds_module import DSModuleBase
 from .module_registry import DSModuleRegistryBase
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 
 def _registry(interface):
 

@@ -89,3 +89,22 @@ class MonitorMaster(Monitor):
     def write_events(self, event_list):
         for m in self.monitors:
             m.write_events(event_list)
+
+
+def check_tb_availability():
+    """Raise ImportError unless a TensorBoard writer can be created."""
+    try:
+        from torch.utils.tensorboard import SummaryWriter  # noqa: F401
+    except ImportError:
+        print("If you want to use tensorboard logging, please `pip install tensorboard`")
+        raise
+
+
+def check_wandb_availability():
+    try:
+        import wandb  # noqa: F401
+    except ImportError:
+        print('If you want to use wandb logging, please `pip install wandb` and follow the instructions at '
+              'https://docs.wandb.ai/quickstart')
+        raise
+

@@ -16,6 +16,8 @@ import torch.nn.functional as F
 
 from . import flash_small as FS
 
+__path__ = []  # lets the reference's per-class sub-paths resolve through `_import_paths`
+
 
 def _check_shapes(Q, biases):
     B, N, S, H, D = Q.shape
