@@ -91,6 +91,13 @@ PATHS = {
                                                        {"DeepSpeedDiffusersAttention": "DSDiffusersAttention"})],
     "ops.transformer.inference.diffusers_transformer_block": [
         ("module_inject.diffusers", {"DeepSpeedDiffusersTransformerBlock": "DSDiffusersTransformerBlock"})],
+    **{f"module_inject.containers.{f}": [("module_inject.containers", "*")]
+       for f in ("base", "base_moe", "bert", "bloom", "clip", "distil_bert", "gpt2", "gptj", "gptneo", "gptneox",
+                 "internlm", "llama", "llama2", "megatron_gpt", "megatron_gpt_moe", "opt", "unet", "vae")},
+    "module_inject.replace_policy": [("module_inject.containers", {"replace_policies": "replace_policies",
+                                                                  "generic_policies": "generic_policies"})],
+    "module_inject.utils": [("module_inject.containers", {"policy_to_ds_container": "policy_to_ds_container"})],
+    "module_inject.inject": [("module_inject.containers", {"module_inject": "replace_layers_with_policy"})],
     # ---- inference v1 model wrappers: one fused layer serves every architecture
     "model_implementations.diffusers.unet": [("module_inject.diffusers", {"DSUNet": "DSUNet"})],
     "model_implementations.diffusers.vae": [("module_inject.diffusers", {"DSVAE": "DSVAE"})],

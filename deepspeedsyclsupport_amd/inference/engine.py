@@ -75,7 +75,19 @@ class InferenceEngine(torch.nn.Module):
             if config.replace_with_kernel_inject:
                 raise ValueError("Cannot use both user specified injection policy and kernel injection")
             from ..module_inject.auto_tp import AutoTP
-            AutoTP(model, self.mp_group, self.tp_size, self.tp_rank, injection_policy=self.injection_dict).apply()
+            from ..module_inject.policy import DSPolicy
+            by_policy = {k: v for k, v in self.injection_dict.items()
+                         if isinstance(v, type) and issubclass(v, DSPolicy)}
+            by_names = {k: v for k, v in self.injection_dict.items() if k not in by_policy}
+            if by_policy:
+                # {client layer class: policy class}: every such layer becomes one fused inference layer
+                from ..module_inject.containers import replace_layers_with_policy
+                model = model.to(self.device)
+                self.policy_injected = sum(
+                    replace_layers_with_policy(model, layer_cls, policy_cls, config, getattr(model, "config", None))
+                    for layer_cls, policy_cls in by_policy.items())
+            if by_names:
+                AutoTP(model, self.mp_group, self.tp_size, self.tp_rank, injection_policy=by_names).apply()
             self.module = model.to(self.device)
             if self.dtype in (torch.float16, torch.bfloat16, torch.float32):
                 self.module = self.module.to(self.dtype)

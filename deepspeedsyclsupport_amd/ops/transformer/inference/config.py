@@ -43,6 +43,7 @@ class DeepSpeedInferenceConfig:
         self.rotate_every_two = rotate_every_two
         self.return_tuple = return_tuple
         self.mlp_after_attn = mlp_after_attn
+        self.shared_parallel_norm = True
         self.mlp_act_func_type = ActivationFuncType(mlp_act_func_type)
         self.training_mp_size = training_mp_size
         self.bigscience_bloom = bigscience_bloom
@@ -89,7 +90,11 @@ class DeepSpeedInferenceConfig:
                            qkv_bias=self.norm_type != NormType.RMSNorm, o_bias=self.norm_type != NormType.RMSNorm,
                            mlp_bias=self.norm_type != NormType.RMSNorm, max_positions=self.max_out_tokens,
                            sliding_window=self.window_size if self.local_attention else 0,
-                           attn_scale=0.0 if self.scale_attention else 1.0)
+                           attn_scale=0.0 if self.scale_attention else 1.0,
+                           # mlp_after_attn=False: attention and MLP both read the layer input and are summed with it
+                           # (GPT-J: off ONE LayerNorm; GPT-NeoX: each off its own -> shared_parallel_norm False)
+                           parallel_residual=not self.mlp_after_attn,
+                           shared_parallel_norm=(not self.mlp_after_attn) and self.shared_parallel_norm)
 
 
 class DeepSpeedMoEInferenceConfig(DeepSpeedInferenceConfig):
