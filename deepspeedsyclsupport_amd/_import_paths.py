@@ -83,6 +83,11 @@ PATHS = {
                                                          {"BertSparseSelfAttention": "BertSparseSelfAttention"})],
     "ops.sparse_attention.sparse_attention_utils": [("ops.sparse_attention.sparse_self_attention",
                                                      {"SparseAttentionUtils": "SparseAttentionUtils"})],
+    "ops.transformer.inference.ds_mlp": [("ops.transformer.inference.ds_attention", {"DeepSpeedMLP": "DeepSpeedMLP"})],
+    **{f"ops.transformer.inference.op_binding.{f}": [("ops.transformer.inference.op_binding", {n: n, "BaseOp": "BaseOp"})]
+       for f, n in (("base", "BaseOp"), ("gelu_gemm", "GELUGemmOp"), ("linear", "LinearOp"), ("mlp_gemm", "MLPGemmOp"),
+                    ("qkv_gemm", "QKVGemmOp"), ("residual_add", "ResidualAddOp"), ("softmax", "SoftmaxOp"),
+                    ("softmax_context", "SoftmaxContextOp"), ("vector_matmul", "VectorMatMulOp"))},
     "ops.transformer.inference.bias_add": [("ops.spatial", {"nhwc_bias_add": "nhwc_bias_add"})],
     "ops.transformer.inference.moe_inference": [
         ("ops.transformer.inference.layer", {"DeepSpeedMoEInference": "DeepSpeedMoEInference"}),
@@ -181,6 +186,61 @@ PATHS = {
 
 
 
+def _section_constants(section, model_path, model_name, prefix=None, extra=None):
+    """Names the reference's `constants.py` files define for a config section, derived from the pydantic model that
+    parses it here: SECTION = "section", SECTION_KEY = "key", SECTION_KEY_DEFAULT = default."""
+
+    def build():
+        model = getattr(importlib.import_module(f"{_PKG}.{model_path}"), model_name)
+        pre = (prefix or section).upper()
+        out = {pre: section, f"{pre}_FORMAT": f'"{section}": {{...}}'}
+        for key, field in model.model_fields.items():
+            out[f"{pre}_{key.upper()}"] = key
+            if not field.is_required():
+                out[f"{pre}_{key.upper()}_DEFAULT"] = field.get_default(call_default_factory=True)
+        out.update(extra or {})
+        return out
+
+    return build
+
+
+# reference path -> callable returning the module's names
+GENERATED = {
+    "comm.constants": _section_constants("comms_logger", "runtime.config", "CommsLoggerConfig", extra={
+        "NCCL_BACKEND": "nccl", "CCL_BACKEND": "ccl", "MPI_BACKEND": "mpi", "GLOO_BACKEND": "gloo",
+        "SCCL_BACKEND": "sccl", "HCCL_BACKEND": "hccl", "DEFAULT_AML_MASTER_PORT": "54965",
+        "DEFAULT_AML_NCCL_SOCKET_IFNAME": "^docker0,lo"}),
+    "profiling.constants": _section_constants("flops_profiler", "runtime.config", "FlopsProfilerConfig"),
+    "nebula.constants": _section_constants("nebula", "nebula.config", "DeepSpeedNebulaConfig", extra={
+        "NEBULA_EXPORT_ENVS": ["DLTS_JOB_ID", "DLTS_NUM_WORKER", "NEBULA_PERSISTENT_STORAGE_PATH",
+                               "NEBULA_PERSISTENT_TIME_INTERVAL", "AML_RUN_ID", "AZUREML_RUN_TOKEN",
+                               "AZUREML_WORKSPACE_SCOPE", "AZUREML_EXPERIMENT_SCOPE",
+                               "AZUREML_RUN_HISTORY_SERVICE_ENDPOINT", "AZUREML_RUN_ID", "NEBULA_MEMORY_BUFFER_SIZE",
+                               "AZUREML_PARAMETER_ITPJOB_NAME", "FC_TASKROLE_NAME", "FC_TASK_INDEX",
+                               "MASTER_HOST", "LOCAL_HOST", "AZUREML_BLOB_ACCOUNT_NAME", "AZUREML_BLOB_ACCOUNT_KEY"],
+        "DLTS_POD_ENV_PATH": "/dlts-runtime/env/pod.env"}),
+    "autotuning.constants": _section_constants("autotuning", "autotuning.config", "DeepSpeedAutotuningConfig",
+                                               extra={"AUTOTUNING_METRIC_LATENCY": "latency",
+                                                      "AUTOTUNING_METRIC_THROUGHPUT": "throughput",
+                                                      "AUTOTUNING_METRIC_FLOPS": "flops",
+                                                      "AUTOTUNING_TUNER_GRIDSEARCH": "gridsearch",
+                                                      "AUTOTUNING_TUNER_RANDOM": "random",
+                                                      "AUTOTUNING_TUNER_MODELBASED": "model_based"}),
+    "runtime.swap_tensor.constants": _section_constants("aio", "runtime.config", "AIOConfig"),
+    "elasticity.constants": _section_constants("elasticity", "runtime.config", "ElasticityConfigModel", extra={
+        "ENABLED": "enabled", "ENABLED_DEFAULT": False, "MAX_ACCEPTABLE_BATCH_SIZE": "max_train_batch_size",
+        "MAX_ACCEPTABLE_BATCH_SIZE_DEFAULT": 2000, "MICRO_BATCHES": "micro_batch_sizes",
+        "MICRO_BATCHES_DEFAULT": [2, 4, 6], "MIN_GPUS": "min_gpus", "MIN_GPUS_DEFAULT": 1, "MAX_GPUS": "max_gpus",
+        "MAX_GPUS_DEFAULT": 10000, "NUM_GPUS_PER_NODE": "num_gpus_per_node", "NUM_GPUS_PER_NODE_DEFAULT": 1,
+        "MODEL_PARALLEL_SIZE": "model_parallel_size", "MODEL_PARALLEL_SIZE_DEFAULT": 1, "MIN_TIME": "min_time",
+        "MIN_TIME_DEFAULT": 0, "PREFER_LARGER_BATCH": "prefer_larger_batch", "PREFER_LARGER_BATCH_DEFAULT": True,
+        "IGNORE_NON_ELASTIC_BATCH_INFO": "ignore_non_elastic_batch_info",
+        "IGNORE_NON_ELASTIC_BATCH_INFO_DEFAULT": False, "VERSION": "version",
+        "LATEST_ELASTICITY_VERSION": 0.2, "MINIMUM_DEEPSPEED_VERSION": "0.3.8",
+        "DEEPSPEED_ELASTICITY_CONFIG": "DEEPSPEED_ELASTICITY_CONFIG"}),
+}
+
+
 _VIRTUAL = None
 
 
@@ -189,11 +249,11 @@ def _virtual_packages():
     global _VIRTUAL
     if _VIRTUAL is None:
         _VIRTUAL = set()
-        for key in PATHS:
+        for key in list(PATHS) + list(GENERATED):
             parts = key.split(".")
             for i in range(1, len(parts)):
                 prefix = ".".join(parts[:i])
-                if prefix not in PATHS:
+                if prefix not in PATHS and prefix not in GENERATED:
                     _VIRTUAL.add(prefix)
     return _VIRTUAL
 
@@ -204,7 +264,7 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
         if not fullname.startswith(_PKG + "."):
             return None
         rel = fullname[len(_PKG) + 1:]
-        if rel in PATHS:
+        if rel in PATHS or rel in GENERATED:
             return importlib.machinery.ModuleSpec(fullname, self)
         if rel in _virtual_packages():
             return importlib.machinery.ModuleSpec(fullname, self, is_package=True)
@@ -215,6 +275,11 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
 
     def exec_module(self, module):
         rel = module.__name__[len(_PKG) + 1:]
+        if rel in GENERATED:
+            module.__doc__ = f"Reference constants module `deepspeed.{rel}`, derived from the config model."
+            for k, v in GENERATED[rel]().items():
+                setattr(module, k, v)
+            return
         if rel not in PATHS:     # a directory of the reference's tree that only holds served paths
             module.__path__ = []
             module.__doc__ = f"Reference package `deepspeed.{rel}` (paths below it: `{_PKG}/_import_paths.py`)."

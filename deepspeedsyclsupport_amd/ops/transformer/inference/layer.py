@@ -84,6 +84,19 @@ class DeepSpeedTransformerInference(nn.Module):
 
         return view(k), view(v)
 
+    def _meta(self, B, n, start, fresh):
+        """Batch metadata of a step that appends `n` tokens at position `start` to each of `B` sequences."""
+        if start + n > self.per_seq * self.block_size:
+            raise ValueError(f"sequence length {start + n} exceeds max_out_tokens={self.config.max_out_tokens}")
+        if fresh:
+            self._ensure_cache(B)
+        dev = self.device
+        tables = torch.arange(B * self.per_seq, dtype=torch.int32, device=dev).view(B, self.per_seq)
+        st = torch.full((B, ), start, dtype=torch.int32, device=dev)
+        pos = (st[:, None] + torch.arange(n, dtype=torch.int32, device=dev)[None, :]).reshape(-1).contiguous()
+        return BatchMeta(block_tables=tables, start_pos=st, seq_lens=st + n, pos_ids=pos, n_new=n,
+                         max_len=self.per_seq * self.block_size, prefill_from_zero=start == 0)
+
     @torch.no_grad()
     def forward(self, input=None, input_mask=None, attention_mask=None, attn_mask=None, head_mask=None,
                 layer_past=None, get_key_value=False, get_present=False, encoder_output=None, enc_dec_attn_mask=None,
@@ -99,16 +112,7 @@ class DeepSpeedTransformerInference(nn.Module):
         past = layer_past if layer_past is not None else past_key_value
         B, n, _ = h.shape
         start = 0 if past is None else int(past[0].shape[2])
-        if start + n > self.per_seq * self.block_size:
-            raise ValueError(f"sequence length {start + n} exceeds max_out_tokens={self.config.max_out_tokens}")
-        if past is None:
-            self._ensure_cache(B)
-        dev = self.device
-        tables = torch.arange(B * self.per_seq, dtype=torch.int32, device=dev).view(B, self.per_seq)
-        st = torch.full((B, ), start, dtype=torch.int32, device=dev)
-        pos = (st[:, None] + torch.arange(n, dtype=torch.int32, device=dev)[None, :]).reshape(-1).contiguous()
-        meta = BatchMeta(block_tables=tables, start_pos=st, seq_lens=st + n, pos_ids=pos, n_new=n,
-                         max_len=self.per_seq * self.block_size, prefill_from_zero=start == 0)
+        meta = self._meta(B, n, start, fresh=past is None)
         inp = h.to(self.config.dtype)
         out, residual = self.layer(inp, None, meta, self.cache, self.rope, self.alibi)
         out = (out + residual).to(h.dtype)

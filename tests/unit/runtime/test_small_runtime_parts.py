@@ -105,3 +105,26 @@ def test_reference_paths_resolve(path, names):
     mod = importlib.import_module("deepspeedsyclsupport_amd." + path)
     for n in names:
         assert hasattr(mod, n), (path, n)
+
+
+def test_generated_constants_follow_the_config_models():
+    cc = importlib.import_module("deepspeedsyclsupport_amd.comm.constants")
+    assert cc.COMMS_LOGGER == "comms_logger" and cc.COMMS_LOGGER_ENABLED == "enabled"
+    assert cc.COMMS_LOGGER_ENABLED_DEFAULT is False and cc.NCCL_BACKEND == "nccl"
+    ac = importlib.import_module("deepspeedsyclsupport_amd.autotuning.constants")
+    assert ac.AUTOTUNING_TUNER_TYPE == "tuner_type" and ac.AUTOTUNING_TUNER_TYPE_DEFAULT == "gridsearch"
+    ec = importlib.import_module("deepspeedsyclsupport_amd.elasticity.constants")
+    assert ec.MICRO_BATCHES == "micro_batch_sizes" and ec.LATEST_ELASTICITY_VERSION == 0.2
+
+
+def test_quantization_context_quantizes_modules_built_inside():
+    from deepspeedsyclsupport_amd.inference.quantization.layers import QuantizedLinear
+    from deepspeedsyclsupport_amd.inference.quantization.quantization_context import QuantizationContext
+    cfg = {"weight_quantization": {"quantized_initialization": {"num_bits": 8, "group_size": 32, "group_dim": 1,
+                                                                  "symmetric": False}}}
+    before = torch.nn.Module.__init__
+    with QuantizationContext(config_dict_or_path=cfg):
+        net = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.ReLU(), torch.nn.Linear(64, 32))
+    assert torch.nn.Module.__init__ is before
+    assert isinstance(net[0], QuantizedLinear) and isinstance(net[2], QuantizedLinear)
+    assert net(torch.randn(3, 64)).shape == (3, 32)
