@@ -92,6 +92,8 @@ PATHS = {
     "ops.transformer.inference.moe_inference": [
         ("ops.transformer.inference.layer", {"DeepSpeedMoEInference": "DeepSpeedMoEInference"}),
         ("ops.transformer.inference.config", {"DeepSpeedMoEInferenceConfig": "DeepSpeedMoEInferenceConfig"})],
+    "ops.transformer.inference.diffusers_2d_transformer": [
+        ("module_inject.diffusers", {"Diffusers2DTransformerConfig": "Diffusers2DTransformerConfig"})],
     "ops.transformer.inference.diffusers_attention": [("module_inject.diffusers",
                                                        {"DeepSpeedDiffusersAttention": "DSDiffusersAttention"})],
     "ops.transformer.inference.diffusers_transformer_block": [

@@ -135,6 +135,13 @@ class DSDiffusersAttention(nn.Module):
         return o
 
 
+class Diffusers2DTransformerConfig:
+    """Options of the fused diffusers transformer block (reference `diffusers_2d_transformer.py`)."""
+
+    def __init__(self, int8_quantization=False):
+        self.int8_quantization = int8_quantization
+
+
 class DSDiffusersTransformerBlock(nn.Module):
     """Fused replacement of a LayerNorm `BasicTransformerBlock` (reference `diffusers_transformer_block.py:35-106`):
     LN1 -> self-attention -> (+res, LN2) -> cross-attention -> (+res, LN3) -> GEGLU FF -> (+bias, +res)."""

@@ -145,3 +145,21 @@ def test_sharding_rules():
     assert sharding.sharded_unembed_dim(101, 0, 2) + sharding.sharded_unembed_dim(101, 1, 2) == 101
     with pytest.raises(ValueError):
         sharding.get_shard_endpoints(100, 0, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["llama", "mixtral", "falcon"])
+def test_build_from_checkpoint_directory_gpu(kind, tmp_path):
+    """The streamed policy load into the bf16 device model, prompt + one decode step through the HIP kernels."""
+    m = tiny(kind, H=256).eval()
+    m.save_pretrained(str(tmp_path), safe_serialization=True)
+    eng = build_hf_engine(str(tmp_path), _cfg(), dtype=torch.bfloat16)
+    assert eng.model.layers[0].qkv_w.is_cuda and eng.model.dtype == torch.bfloat16
+    ids = torch.randint(0, m.config.vocab_size, (2, 21), generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        ref_prompt = m(ids[:, :20]).logits[:, -1].float()
+        ref_next = m(ids).logits[:, -1].float()
+    out = eng.put([1, 2], [ids[0, :20], ids[1, :20]]).float().cpu()
+    assert (out - ref_prompt).abs().max().item() < 0.05 * ref_prompt.abs().max().item() + 0.02
+    out = eng.put([1, 2], [ids[0, 20:], ids[1, 20:]]).float().cpu()
+    assert (out - ref_next).abs().max().item() < 0.05 * ref_next.abs().max().item() + 0.02
