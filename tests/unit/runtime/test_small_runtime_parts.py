@@ -128,3 +128,23 @@ def test_quantization_context_quantizes_modules_built_inside():
     assert torch.nn.Module.__init__ is before
     assert isinstance(net[0], QuantizedLinear) and isinstance(net[2], QuantizedLinear)
     assert net(torch.randn(3, 64)).shape == (3, 32)
+
+
+def _ccl_backend():
+    from deepspeedsyclsupport_amd.comm.ccl import CCLBackend
+    be = CCLBackend()
+    assert be.is_initialized() and be.world_size == 2 and "inference_all_reduce" in be.available_coll
+    t = torch.full((5, ), float(be.world_rank + 1))
+    be.all_reduce(t)
+    assert t.tolist() == [3.0] * 5
+    t = torch.full((1024, ), float(be.world_rank + 1))
+    be.inference_all_reduce(t)          # host tensors: the shared-memory reduce when the native extension is there
+    assert t.tolist() == [3.0] * 1024
+    b = torch.arange(4.) if be.world_rank == 0 else torch.zeros(4)
+    be.broadcast(b, 0)
+    assert b.tolist() == [0.0, 1.0, 2.0, 3.0]
+    be.barrier()
+
+
+def test_ccl_backend_object():
+    run_distributed(_ccl_backend, 2)
