@@ -117,3 +117,57 @@ def ds_quantizer(input, groups=1, bit_num=8, sr=False, asym=False):
     """Reference signature: quantise `input` into `groups` groups in place (fake quant)."""
     gs = input.numel() // groups
     return fake_quantize(input, gs, bit_num, not asym, sr)
+
+
+# ---- the quantizer extension's function names (reference `csrc/quantization/pt_binding.cpp:270-297`)
+def ds_quantize_fp32(vals, groups, bits):
+    """In-place symmetric fake quantisation of `vals` in `groups` groups (fp16 / bf16 / fp32 alike here)."""
+    return ds_quantizer(vals, groups, bits)
+
+
+def ds_sr_quantize_fp32(vals, groups, bits):
+    return ds_quantizer(vals, groups, bits, sr=True)
+
+
+def ds_quantize_asym_fp32(vals, groups, bits):
+    return ds_quantizer(vals, groups, bits, asym=True)
+
+
+def ds_sr_quantize_asym_fp32(vals, groups, bits):
+    return ds_quantizer(vals, groups, bits, sr=True, asym=True)
+
+
+ds_quantize_fp16, ds_sr_quantize_fp16 = ds_quantize_fp32, ds_sr_quantize_fp32
+ds_quantize_asym_fp16, ds_sr_quantize_asym_fp16 = ds_quantize_asym_fp32, ds_sr_quantize_asym_fp32
+
+
+def dequantize_int8_to_half_experimental(data, scales_and_zeros, num_group, group_size):
+    """Asymmetric int8 codes [num_group * group_size] + [num_group, 2] (scale, minimum) -> fp16."""
+    x = data.reshape(num_group, group_size).float()
+    sz = scales_and_zeros.reshape(num_group, 2).float()
+    return (x * sz[:, :1] + sz[:, 1:]).to(torch.float16).reshape(-1)
+
+
+def dequantize_int4_to_half_experimental(data, scales_and_zeros, num_group, group_size):
+    """Packed asymmetric int4 codes (two per byte, high nibble first) + (scale, minimum) per group -> fp16."""
+    b = data.reshape(-1).to(torch.uint8)
+    codes = torch.stack([(b >> 4) & 0xF, b & 0xF], dim=1).reshape(-1)
+    return dequantize_int8_to_half_experimental(codes, scales_and_zeros, num_group, group_size)
+
+
+def swizzle_quant(input_vals, groups, num_bits, quant_type=None, pipeline_size=1, nodes=1, devices_per_node=1):
+    """Quantise with the destination chunks re-ordered [local index][node] (qgZ first level). Returns (codes,
+    scales)."""
+    from ...runtime.zero.zeropp import swizzle_quant as _sw
+    qt = _sw(input_vals.reshape(-1), nodes, devices_per_node, input_vals.numel() // groups, num_bits)
+    return qt.data, qt.scales
+
+
+def quantized_reduction(input_vals, input_scales, in_groups, out_groups, num_bits, quant_type=None,
+                        devices_per_node=1):
+    """Dequantise `devices_per_node` stacked copies, sum, re-quantise (qgZ second step). Returns (codes, scales)."""
+    from ...runtime.zero.zeropp import quantized_reduction as _qr
+    gs = input_vals.numel() // in_groups
+    qt = _qr(input_vals.reshape(-1), input_scales.reshape(-1), devices_per_node, gs, num_bits)
+    return qt.data, qt.scales
+

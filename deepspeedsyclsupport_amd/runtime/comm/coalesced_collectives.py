@@ -57,10 +57,16 @@ def all_to_all_quant_reduce(tensors: List[Tensor], groups: Dict = None) -> List[
     reduce-scatter; matrices are exchanged as int8 blocks through one all-to-all and summed by the fused
     dequantise-reduce kernel (`runtime/zero/zeropp.py`). One xGMI node is a single level: `groups` may carry the
     group to use under the key "world" (default: all ranks); the reference's two-level intra / inter-node split is
-    not needed on a fully connected node."""
-    from ..zero.zeropp import quantized_reduce_scatter
-    group = (groups or {}).get("world")
+    not needed on a fully connected node; when `groups` is the reference's table (`local_<node>`, `global_<local
+    index>`, as `parallel.groups._get_local_all_to_all_group()` builds it) and it spans several nodes, the exchange runs
+    in two levels (`zeropp.quantized_reduce_scatter_2level`)."""
+    from ..zero.zeropp import quantized_reduce_scatter, quantized_reduce_scatter_2level
+    groups = groups or {}
+    group = groups.get("world")
     world = dist.get_world_size(group)
+    # the reference's group table (`local_<node>` / `global_<local index>`): two levels when it spans several nodes
+    from ..zero.zeropp import levels_from_table
+    levels = levels_from_table(groups)
     out: List[Tensor] = [None] * len(tensors)
     for i, t in enumerate(tensors):
         if t.dim() == 1 or t.numel() % (world * 64):
@@ -68,6 +74,9 @@ def all_to_all_quant_reduce(tensors: List[Tensor], groups: Dict = None) -> List[
             continue
         seg = t.numel() // world
         buf = torch.empty(seg, dtype=torch.float32, device=t.device)
-        quantized_reduce_scatter(buf, t.reshape(-1), group)
+        if levels is not None:
+            quantized_reduce_scatter_2level(buf, t.reshape(-1), *levels)
+        else:
+            quantized_reduce_scatter(buf, t.reshape(-1), group)
         out[i] = buf.div_(world).to(t.dtype)
     return out

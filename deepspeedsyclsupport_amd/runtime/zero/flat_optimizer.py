@@ -694,8 +694,15 @@ class FlatZeroOptimizer(ZeROOptimizer):
             elif g.partition:
                 out = torch.empty(g.seg, dtype=comm.dtype, device=comm.device)
                 if self.zc is not None and self.zc.zero_quantized_gradients:
-                    from .zeropp import quantized_reduce_scatter  # qgZ: int8 all-to-all + fused dequant-reduce
-                    quantized_reduce_scatter(out, comm, g.dp_group)
+                    # qgZ: int8 all-to-all + fused dequant-reduce; two levels (inside the node, then between
+                    # nodes) when the group spans several nodes
+                    from .zeropp import qgz_groups, quantized_reduce_scatter, quantized_reduce_scatter_2level
+                    if not hasattr(self, "_qgz_levels"):
+                        self._qgz_levels = qgz_groups(g.dp_group)
+                    if self._qgz_levels is not None:
+                        quantized_reduce_scatter_2level(out, comm, *self._qgz_levels)
+                    else:
+                        quantized_reduce_scatter(out, comm, g.dp_group)
                 else:
                     dist.reduce_scatter_tensor(out, comm, group=g.dp_group)
                 if self.mics_replica_group is not None and g.dp_group is self.mics_shard_group:

@@ -59,6 +59,72 @@ def quantized_reduce_scatter(out, inp, group, bits=8):
     return out
 
 
+def swizzle_quant(inp, nodes, local, group_size, bits=8):
+    """Quantise a flat gradient of `nodes * local` destination chunks with the chunks re-ordered
+    [local index][node] instead of [node][local index] (reference `swizzled_quantize.cu:21`): what goes to local
+    peer b — the chunks of every node's rank b — becomes one contiguous run, so the intra-node all-to-all needs no
+    gather. Returns the QuantizedTensor of the re-ordered data."""
+    seg = inp.numel() // (nodes * local)
+    sw = inp.view(nodes, local, seg).transpose(0, 1).contiguous().view(-1)
+    return quantize(sw, group_size=group_size, bits=bits, symmetric=True)
+
+
+def quantized_reduction(q, scales, nsrc, group_size, bits=8):
+    """Dequantise `nsrc` stacked copies, sum them, re-quantise the sum (reference `quant_reduce.cu:21`: the
+    intra-node step of the two-level exchange). Returns a QuantizedTensor of numel / nsrc elements."""
+    red = dequant_reduce(q, scales, nsrc, group_size, 1.0, dtype=torch.float32)
+    return quantize(red.view(-1), group_size=group_size, bits=bits, symmetric=True)
+
+
+@torch.no_grad()
+def quantized_reduce_scatter_2level(out, inp, local_group, global_group, bits=8):
+    """qgZ across nodes (reference `coalesced_collectives.py:31-68`): out[seg] <- sum over ALL ranks of this rank's
+    chunk of inp[nodes * local * seg], moving only 1 / local of the single-level volume between nodes.
+
+    rank = node * local + b (consecutive ranks share a node). Step 1, inside the node (xGMI all-to-all): peer b
+    receives, from each of the node's ranks, the chunks destined for the ranks with local index b on every node, and
+    sums them (fused dequant-reduce) — `nodes` partial chunks. Step 2, between nodes (ranks with the same local
+    index): partial chunk a goes to node a; the `nodes` partials of this rank's own chunk are summed into `out`.
+    """
+    local = dist.get_world_size(local_group)
+    nodes = dist.get_world_size(global_group)
+    seg = out.numel()
+    if inp.numel() != nodes * local * seg:
+        raise ValueError(f"input of {inp.numel()} elements is not nodes * local * segment = {nodes * local * seg}")
+    gs = _qgroup(seg)
+    qt = swizzle_quant(inp.reshape(-1), nodes, local, gs, bits)
+    q1, s1 = torch.empty_like(qt.data), torch.empty_like(qt.scales)
+    dist.all_to_all_single(q1, qt.data, group=local_group)
+    dist.all_to_all_single(s1, qt.scales, group=local_group)
+    part = quantized_reduction(q1, s1, local, gs, bits)              # [nodes * seg]: this node's sums, by target node
+    q2, s2 = torch.empty_like(part.data), torch.empty_like(part.scales)
+    dist.all_to_all_single(q2, part.data, group=global_group)
+    dist.all_to_all_single(s2, part.scales, group=global_group)
+    out.copy_(dequant_reduce(q2, s2, nodes, gs, 1.0, dtype=torch.float32).view(-1))
+    return out
+
+
+def qgz_groups(dp_group):
+    """(local group, cross-node group) for a two-level exchange over `dp_group`, or None when the group sits on one
+    node (or is not the whole job, where the node split is unknown): then the single-level exchange is used."""
+    from ...parallel import groups
+    world = dist.get_world_size()
+    if dist.get_world_size(dp_group) != world:
+        return None
+    return levels_from_table(groups._get_local_all_to_all_group())
+
+
+def levels_from_table(table):
+    """This rank's (local, cross-node) groups out of the `local_<node>` / `global_<local index>` table, or None when
+    the table holds one node. (A group's size can only be asked by its members, so the rank's own groups are found
+    by membership.)"""
+    local = next((g for k, g in table.items() if k.startswith("local_") and dist.get_rank(g) >= 0), None)
+    cross = next((g for k, g in table.items() if k.startswith("global_") and dist.get_rank(g) >= 0), None)
+    if local is None or cross is None or dist.get_world_size(cross) < 2:
+        return None
+    return local, cross
+
+
 class HpzState:
     """Secondary (intra-node) partitions for hpZ."""
 
