@@ -16,8 +16,10 @@ _PKG = __name__.rsplit(".", 1)[0]
 
 # reference path (below the package) -> [(real module (below the package), {exposed name: real name} or "*")]
 PATHS = {
-    "runtime.zero.stage3": [("runtime.zero.flat_optimizer", {"DeepSpeedZeroOptimizer_Stage3": "DeepSpeedZeroOptimizer_Stage3"})],
-    "runtime.zero.stage_1_and_2": [("runtime.zero.flat_optimizer", {"DeepSpeedZeroOptimizer": "DeepSpeedZeroOptimizer"})],
+    "runtime.zero.stage3": [("runtime.zero.flat_optimizer", {"DeepSpeedZeroOptimizer_Stage3": "DeepSpeedZeroOptimizer_Stage3",
+                                                            "estimate_zero3_model_states_mem_needs": "estimate_zero3_model_states_mem_needs", "estimate_zero3_model_states_mem_needs_all_live": "estimate_zero3_model_states_mem_needs_all_live", "estimate_zero3_model_states_mem_needs_all_cold": "estimate_zero3_model_states_mem_needs_all_cold", "model_to_params": "model_to_params"})],
+    "runtime.zero.stage_1_and_2": [("runtime.zero.flat_optimizer", {"DeepSpeedZeroOptimizer": "DeepSpeedZeroOptimizer",
+                                                                   "estimate_zero2_model_states_mem_needs": "estimate_zero2_model_states_mem_needs", "estimate_zero2_model_states_mem_needs_all_live": "estimate_zero2_model_states_mem_needs_all_live", "estimate_zero2_model_states_mem_needs_all_cold": "estimate_zero2_model_states_mem_needs_all_cold", "model_to_params": "model_to_params"})],
     "runtime.zero.partitioned_param_coordinator": [("runtime.zero.coordinator",
                                                     {"PartitionedParameterCoordinator": "ParamCoordinator"})],
     "runtime.zero.parameter_offload": [("runtime.zero.coordinator", {"DeepSpeedZeRoOffload": "ParamCoordinator"})],

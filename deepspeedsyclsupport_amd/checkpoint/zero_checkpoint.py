@@ -498,3 +498,13 @@ def layouts_match(saved, current):
         if [tuple(r) for r in a["runs"]] != [tuple(r) for r in b["runs"]]:
             return False
     return True
+
+
+def __getattr__(name):
+    # `ZeROCheckpoint` (folder inspection / contraction) lives with `DeepSpeedCheckpoint`; resolved lazily because
+    # that module imports this one
+    if name == "ZeROCheckpoint":
+        from .deepspeed_checkpoint import ZeROCheckpoint
+        return ZeROCheckpoint
+    raise AttributeError(name)
+

@@ -438,3 +438,51 @@ def log_summary(show_straggler=False):
     if get_rank() == 0:
         comms_logger.log_all(print_log=True, show_straggler=show_straggler)
     barrier()
+
+
+# ------------------------------------------------------------------------------------------------ backend object
+def get_local_rank_from_launcher():
+    return int(os.environ.get("LOCAL_RANK", os.environ.get("OMPI_COMM_WORLD_LOCAL_RANK", 0)))
+
+
+def get_world_rank_from_launcher():
+    return int(os.environ.get("RANK", os.environ.get("OMPI_COMM_WORLD_RANK", 0)))
+
+
+def get_world_size_from_launcher():
+    return int(os.environ.get("WORLD_SIZE", os.environ.get("OMPI_COMM_WORLD_SIZE", 1)))
+
+
+class TorchBackend:
+    """torch.distributed as a backend object (reference `comm/torch.py:99`): every collective of this module as a
+    method, for code that holds a backend instead of calling the module functions."""
+
+    def __init__(self, backend=None, timeout=default_pg_timeout, init_method=None, rank=-1, world_size=-1,
+                 name="torch"):
+        self.name = name
+        self.single_gpu_mode = True
+        if not is_initialized():
+            init_distributed(dist_backend=backend, timeout=timeout, init_method=init_method, rank=rank,
+                             world_size=world_size)
+        self.using_mpi = False
+        self.initialized = True
+
+    def is_initialized(self):
+        return is_initialized()
+
+    def has_all_gather_into_tensor(self):
+        return hasattr(tdist, "all_gather_into_tensor")
+
+    def has_reduce_scatter_tensor(self):
+        return hasattr(tdist, "reduce_scatter_tensor")
+
+    def has_all_reduce_coalesced(self):
+        return has_all_reduce_coalesced()
+
+    def __getattr__(self, name):
+        # every collective / query of this module (all_reduce, all_gather_into_tensor, get_rank, new_group, ...)
+        fn = globals().get(name)
+        if callable(fn) and not name.startswith("_"):
+            return fn
+        raise AttributeError(name)
+

@@ -134,3 +134,19 @@ class DeepSpeedInferenceConfig(DeepSpeedConfigModel):
             self.tensor_parallel.tp_size = self.mp_size
         if self.mpu is not None and self.tensor_parallel.mpu is None:
             self.tensor_parallel.mpu = self.mpu
+
+
+from enum import Enum  # noqa: E402
+
+from .v2.inference_utils import DtypeEnum  # noqa: E402,F401  (the multi-spelling dtype enum)
+
+
+class MoETypeEnum(str, Enum):
+    residual = "residual"
+    standard = "standard"
+
+
+class QuantTypeEnum(str, Enum):
+    asym = "asymmetric"
+    sym = "symmetric"
+

@@ -74,6 +74,27 @@ def parse_core_list(spec):
     return out
 
 
+def terminate_process_tree(pid):
+    """SIGTERM a process and all its descendants; SIGKILL whatever is still alive after 30 s."""
+    import psutil
+    try:
+        root = psutil.Process(pid)
+    except psutil.NoSuchProcess:
+        return
+    procs = root.children(recursive=True) + [root]
+    for p in procs:
+        try:
+            p.terminate()
+        except psutil.NoSuchProcess:
+            pass
+    _, alive = psutil.wait_procs(procs, timeout=30)
+    for p in alive:
+        try:
+            p.kill()
+        except psutil.NoSuchProcess:
+            pass
+
+
 def build_rank_envs(world_info, node_rank, master_addr, master_port):
     """Per-local-rank environment dicts for this node (pure; unit-tested)."""
     hosts = list(world_info.keys())

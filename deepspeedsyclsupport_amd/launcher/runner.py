@@ -124,6 +124,21 @@ def parse_inclusion_exclusion(resource_pool, inclusion, exclusion):
     return parse_resource_filter(active, include_str=inclusion, exclude_str=exclusion)
 
 
+def parse_num_nodes(str_num_nodes: str, elastic_training: bool):
+    """`--num_nodes` as (min, max): "4" -> (4, -1); "2:8" (elastic training only) -> (2, 8)."""
+    parts = str(str_num_nodes).split(":")
+    if len(parts) == 1:
+        return int(parts[0]), -1
+    if len(parts) == 2 and elastic_training:
+        lo, hi = int(parts[0]), int(parts[1])
+        if lo < 1 or hi < lo:
+            raise RuntimeError("MIN:MAX format of num_nodes needs 1 <= MIN <= MAX")
+        return lo, hi
+    if len(parts) == 2:
+        raise RuntimeError("MIN:MAX format is only supported in elastic training")
+    raise RuntimeError(f"num_nodes {str_num_nodes} is not in MIN:MAX format")
+
+
 def encode_world_info(world_info):
     return base64.urlsafe_b64encode(json.dumps(world_info).encode("utf-8")).decode("utf-8")
 

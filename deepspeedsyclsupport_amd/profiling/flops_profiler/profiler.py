@@ -73,6 +73,7 @@ class FlopsProfiler:
             if ignore and isinstance(m, ignore):
                 continue
             self._names[id(m)] = name or self.model.__class__.__name__
+            m._ds_flops_profiler = self
 
             def pre(mod, inp):
                 acc.synchronize()
@@ -188,3 +189,32 @@ def get_model_profile(model, input_shape=None, args=None, kwargs=None, print_pro
     if as_string:
         return flops_to_string(flops), macs_to_string(macs), params_to_string(params)
     return flops, macs, params
+
+
+def bytes_to_string(num, units=None, precision=2):
+    return number_to_string(num, units=units, precision=precision) + "B"
+
+
+def _profiler_of(module):
+    prof = getattr(module, "_ds_flops_profiler", None)
+    if prof is None:
+        raise ValueError("the module is not being profiled: start a FlopsProfiler on its model first")
+    return prof
+
+
+def get_module_flops(module):
+    """Forward FLOPs recorded for `module` (its sub-modules included) by the active profiler."""
+    prof = _profiler_of(module)
+    name = prof._names.get(id(module))
+    root = prof.model.__class__.__name__
+    counts = prof._module_flops()    # keyed "<RootClass>.<qualified name>" (the root itself: "<RootClass>")
+    return int(counts.get(name if module is prof.model else f"{root}.{name}", 0))
+
+
+def get_module_macs(module):
+    return get_module_flops(module) // 2
+
+
+def get_module_duration(module):
+    """Forward wall time of `module` in seconds (device-synchronised around the module)."""
+    return float(_profiler_of(module)._durations.get(id(module), 0.0))

@@ -35,6 +35,44 @@ def _version():
     return __version__
 
 
+def split_half_float_double_sparse(tensors):
+    """Bucket gradients by dtype for the plain data-parallel reduction: [(dtype name, [tensors])], sparse
+    gradients in a bucket of their own (reference `engine.py:121-141`)."""
+    from .sparse_tensor import SparseTensor
+    buckets = {}
+    for t in tensors:
+        key = SparseTensor.type() if isinstance(t, SparseTensor) else t.type()
+        buckets.setdefault(key, []).append(t)
+    return list(buckets.items())
+
+
+class EngineTimers:
+    """Which wall-clock timers the engine reports (reference `engine.py:144-176`): micro-step and global timers of
+    forward / backward / reduce / step, all empty when timing is off."""
+
+    def __init__(self, enable_micro_timers, enable_global_timers):
+        from ..utils import timer as T
+        self.forward_timers, self.backward_timers = [], []
+        self.backward_inner_timers, self.backward_reduce_timers = [], []
+        self.step_timers, self.global_timers, self.micro_timers = [], [], []
+        if enable_micro_timers:
+            self.forward_timers += [T.FORWARD_MICRO_TIMER]
+            self.backward_timers += [T.BACKWARD_MICRO_TIMER]
+            self.backward_inner_timers += [T.BACKWARD_INNER_MICRO_TIMER]
+            self.backward_reduce_timers += [T.BACKWARD_REDUCE_MICRO_TIMER]
+            self.step_timers += [T.STEP_MICRO_TIMER]
+            self.micro_timers += [T.FORWARD_MICRO_TIMER, T.BACKWARD_MICRO_TIMER, T.BACKWARD_INNER_MICRO_TIMER,
+                                  T.BACKWARD_REDUCE_MICRO_TIMER, T.STEP_MICRO_TIMER]
+        if enable_global_timers:
+            self.forward_timers += [T.FORWARD_GLOBAL_TIMER]
+            self.backward_timers += [T.BACKWARD_GLOBAL_TIMER]
+            self.backward_inner_timers += [T.BACKWARD_INNER_GLOBAL_TIMER]
+            self.backward_reduce_timers += [T.BACKWARD_REDUCE_GLOBAL_TIMER]
+            self.step_timers += [T.STEP_GLOBAL_TIMER]
+            self.global_timers += [T.FORWARD_GLOBAL_TIMER, T.BACKWARD_GLOBAL_TIMER, T.BACKWARD_INNER_GLOBAL_TIMER,
+                                   T.BACKWARD_REDUCE_GLOBAL_TIMER, T.STEP_GLOBAL_TIMER]
+
+
 class DeepSpeedEngine(nn.Module):
 
     def __init__(self, args, model, optimizer=None, model_parameters=None, training_data=None, lr_scheduler=None,

@@ -223,3 +223,92 @@ def add_tuning_arguments(parser):
     group.add_argument("--warmup_num_steps", type=int, default=1000)
     group.add_argument("--warmup_type", type=str, default=WARMUP_LOG_RATE)
     return parser
+
+
+# ------------------------------------------------------------------------------------------------ command-line glue
+_CLI_KEYS = {
+    LR_RANGE_TEST: ("lr_range_test_min_lr", "lr_range_test_step_rate", "lr_range_test_step_size",
+                    "lr_range_test_staircase"),
+    ONE_CYCLE: ("cycle_first_step_size", "cycle_first_stair_count", "cycle_second_step_size",
+                "cycle_second_stair_count", "decay_step_size", "cycle_min_lr", "cycle_max_lr", "decay_lr_rate",
+                "cycle_min_mom", "cycle_max_mom", "decay_mom_rate"),
+    WARMUP_LR: ("warmup_min_lr", "warmup_max_lr", "warmup_num_steps", "warmup_type"),
+    WARMUP_DECAY_LR: ("warmup_min_lr", "warmup_max_lr", "warmup_num_steps", "warmup_type", "total_num_steps"),
+    WARMUP_COSINE_LR: ("warmup_min_ratio", "warmup_num_steps", "warmup_type", "total_num_steps", "cos_min_ratio"),
+}
+
+
+def parse_arguments():
+    """Parser with the convergence-tuning flags; returns (known args, remaining argv)."""
+    import argparse
+    parser = add_tuning_arguments(argparse.ArgumentParser())
+    return parser.parse_known_args()
+
+
+def override_params(args, params):
+    """Copy every schedule flag that `args` carries (and is not None) into the schedule's parameter dict."""
+    for keys in _CLI_KEYS.values():
+        for k in keys:
+            v = getattr(args, k, None)
+            if v is not None:
+                params[k] = v
+
+
+def override_lr_range_test_params(args, params):
+    for k in _CLI_KEYS[LR_RANGE_TEST]:
+        if getattr(args, k, None) is not None:
+            params[k] = getattr(args, k)
+
+
+def override_1cycle_params(args, params):
+    for k in _CLI_KEYS[ONE_CYCLE]:
+        if getattr(args, k, None) is not None:
+            params[k] = getattr(args, k)
+
+
+def override_warmupLR_params(args, params):
+    for k in _CLI_KEYS[WARMUP_LR]:
+        if getattr(args, k, None) is not None:
+            params[k] = getattr(args, k)
+
+
+def get_config_from_args(args):
+    """({"type": schedule, "params": {...}}, None) from command-line flags, or (None, reason)."""
+    name = getattr(args, "lr_schedule", None)
+    if name is None:
+        return None, "--lr_schedule not specified on command line"
+    if name not in VALID_LR_SCHEDULES:
+        return None, f"{name} is not supported LR schedule"
+    params = {}
+    for k in _CLI_KEYS[name]:
+        if getattr(args, k, None) is not None:
+            params[k] = getattr(args, k)
+    return {"type": name, "params": params}, None
+
+
+def get_lr_from_config(config):
+    """(starting learning rate, "") of a schedule config, or (None, reason)."""
+    if "type" not in config:
+        return None, "LR schedule type not defined in config"
+    if "params" not in config:
+        return None, "LR schedule params not defined in config"
+    name, params = config["type"], config["params"]
+    if name not in VALID_LR_SCHEDULES:
+        return None, f"{name} is not a valid LR schedule"
+    if name == LR_RANGE_TEST:
+        return params.get("lr_range_test_min_lr", 1e-3), ""
+    if name == ONE_CYCLE:
+        return params.get("cycle_max_lr", 0.1), ""
+    return params.get("warmup_max_lr", 0.001), ""
+
+
+def get_torch_optimizer(optimizer):
+    """The torch optimizer behind an optimizer wrapper (ZeRO / fp16 wrappers keep it as `.optimizer`)."""
+    import torch
+    if isinstance(optimizer, torch.optim.Optimizer):
+        return optimizer
+    inner = getattr(optimizer, "optimizer", None)
+    if isinstance(inner, torch.optim.Optimizer):
+        return inner
+    raise TypeError(f"{type(optimizer).__name__} is not a subclass of torch.optim.Optimizer")
+

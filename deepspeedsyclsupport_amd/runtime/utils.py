@@ -211,3 +211,149 @@ def get_only_unique_item(items):
     if len(s) != 1:
         raise RuntimeError(f"expected exactly one unique item, got {s}")
     return s.pop()
+
+
+# ------------------------------------------------------------------------------------------------ small helpers
+class DummyOptim:
+    """Placeholder optimizer over the model's parameters when the client trains without one (reference
+    `runtime/utils.py:DummyOptim`): gives ZeRO a param_groups list to partition."""
+
+    def __init__(self, params):
+        self.param_groups = [{"params": list(params)}]
+
+
+class noop_context:
+    """`with noop_context():` does nothing (stands in for optional contexts)."""
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def required_torch_version(min_version=None, max_version=None):
+    from packaging import version as V
+    cur = V.parse(torch.__version__.split("+")[0])
+    if min_version is not None and cur < V.parse(str(min_version)):
+        return False
+    if max_version is not None and cur > V.parse(str(max_version)):
+        return False
+    return True
+
+
+def bwc_tensor_model_parallel_rank(mpu=None):
+    """Tensor-model-parallel rank from whichever accessor the client's `mpu` has (old and new Megatron names)."""
+    if mpu is None:
+        return 0
+    for name in ("get_tensor_model_parallel_rank", "get_slice_parallel_rank", "get_model_parallel_rank"):
+        if hasattr(mpu, name):
+            return getattr(mpu, name)()
+    return 0
+
+
+def move_to_device(item, device, criterion_func=None):
+    """Move every tensor inside a nested list / tuple / dict (for which `criterion_func` holds) to `device`."""
+    ok = criterion_func or (lambda t: True)
+    if torch.is_tensor(item):
+        return item.to(device) if ok(item) else item
+    if isinstance(item, (list, tuple)):
+        return type(item)(move_to_device(v, device, criterion_func) for v in item)
+    if isinstance(item, dict):
+        return {k: move_to_device(v, device, criterion_func) for k, v in item.items()}
+    return item
+
+
+def copy_to_device(item, device, criterion_func=None):
+    """As `move_to_device` but always a fresh copy (the source keeps its storage)."""
+    ok = criterion_func or (lambda t: True)
+    if torch.is_tensor(item):
+        return item.detach().clone().to(device) if ok(item) else item
+    if isinstance(item, (list, tuple)):
+        return type(item)(copy_to_device(v, device, criterion_func) for v in item)
+    if isinstance(item, dict):
+        return {k: copy_to_device(v, device, criterion_func) for k, v in item.items()}
+    return item
+
+
+def get_global_norm(norm_list):
+    """2-norm of a list of 2-norms."""
+    return float(sum(float(n)**2 for n in norm_list))**0.5
+
+
+def clip_tensors_by_global_norm(input_tensors, max_norm=1.0, global_norm=None, mpu=None, eps=1e-6, use_graph=False):
+    """Scale the tensors in place so their joint 2-norm is at most `max_norm`; returns the norm before clipping."""
+    if global_norm is None:
+        global_norm = get_global_norm_of_tensors(input_tensors, mpu=mpu, use_graph=use_graph)
+    clip = float(max_norm) / (float(global_norm) + eps)
+    if clip < 1.0:
+        for t in input_tensors:
+            t.detach().mul_(clip)
+    return global_norm
+
+
+def clip_gradients(parameters, max_norm=1.0, global_grad_norm=None, mpu=None, eps=1e-6):
+    """Clip `.grad` of the parameters by their (given or computed) global norm; returns that norm."""
+    grads = [p.grad for p in parameters if p.grad is not None]
+    if global_grad_norm is None:
+        global_grad_norm = get_global_norm_of_tensors(grads, mpu=mpu)
+    clip = float(max_norm) / (float(global_grad_norm) + eps)
+    if clip < 1.0:
+        for g in grads:
+            g.detach().mul_(clip)
+    return global_grad_norm
+
+
+def empty_cache():
+    from ..accelerator import get_accelerator
+    get_accelerator().empty_cache()
+    get_accelerator().reset_peak_memory_stats()
+
+
+def get_ma_status():
+    from ..accelerator import get_accelerator
+    from .. import comm as dist
+    if dist.is_initialized() and dist.get_rank() != 0:
+        return 0
+    return get_accelerator().memory_allocated()
+
+
+_mem_alloced = 0
+_mem_cached = 0
+
+
+def memory_status(msg, print_rank=-1, reset_max=False):
+    """One line with allocated / cached device memory and their change since the last call."""
+    global _mem_alloced, _mem_cached
+    from ..accelerator import get_accelerator
+    from .. import comm as dist
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if print_rank != -1 and rank != print_rank:
+        return
+    acc = get_accelerator()
+    acc.synchronize()
+    if reset_max:
+        acc.reset_max_memory_cached()
+        acc.reset_max_memory_allocated()
+    new_a, new_c = acc.memory_allocated(), acc.memory_cached()
+    da, dc = new_a - _mem_alloced, new_c - _mem_cached
+    _mem_alloced, _mem_cached = new_a, new_c
+    gb = 1024**3
+    print(f"RANK={rank} MEMSTATS {msg} device={acc.current_device_name()} current alloc={new_a / gb:0.4f}GB "
+          f"(delta={da / gb:0.4f}GB max={acc.max_memory_allocated() / gb:0.4f}GB) current cache={new_c / gb:0.4f}GB "
+          f"(delta={dc / gb:0.4f}GB max={acc.max_memory_cached() / gb:0.4f}GB)")
+
+
+def prefix_sum_inc(weights):
+    """Inclusive prefix sum of a list."""
+    out, run = [], 0
+    for w in weights:
+        run += w
+        out.append(run)
+    return out
+
+
+def get_inactive_params(param_list):
+    """ZeRO-3 parameters of the list that are not gathered at the moment."""
+    return [p for p in param_list if getattr(p, "ds_status", None) is not None and p.numel() == 0]
+

@@ -1218,6 +1218,35 @@ class FlatZeroOptimizer(ZeROOptimizer):
     def get_local_fp32_param(self, p):
         return self._local_fragment(p, "fp32")
 
+    @torch.no_grad()
+    def set_local_fragment(self, p, value, key):
+        """Write back what `_local_fragment(p, key)` returned (same flat element order): this rank's part only, no
+        collective."""
+        self.join_offload()
+        g, i = self.param_group[id(p)]
+        a, n = g.offsets[i], g.numels[i]
+        flat = value.reshape(-1).to(torch.float32)
+        if g.frozen:
+            lo, hi = max(g.seg_lo, a), min(g.seg_lo + g.seg, a + n)
+            if key == "fp32" and lo < hi:
+                g.shard[lo - g.seg_lo:hi - g.seg_lo].copy_(flat[:hi - lo])
+            return
+        off = 0
+        for run in g.runs:
+            lo, hi = g.seg_lo + run[0], g.seg_lo + run[1]
+            x0, x1 = max(lo, a), min(hi, a + n)
+            if x0 < x1:
+                self._run_write(g, run, key, x0 - g.seg_lo, flat[off:off + x1 - x0], also_shard=key == "fp32")
+                off += x1 - x0
+        if off != flat.numel():
+            raise ValueError(f"local fragment has {off} elements on this rank, got {flat.numel()}")
+
+    def set_local_fp32_param(self, p, value):
+        self.set_local_fragment(p, value, "fp32")
+
+    def set_local_optimizer_state(self, p, value, key):
+        self.set_local_fragment(p, value, key)
+
     def get_local_optimizer_state(self, p, key):
         return self._local_fragment(p, key)
 
@@ -1460,3 +1489,103 @@ class BF16_Optimizer(FlatZeroOptimizer):
 
 class FP16_Optimizer(FlatZeroOptimizer):
     """fp16 params + fp32 master + dynamic loss scale (reference `runtime/fp16/fused_optimizer.py:31`)."""
+
+
+# ------------------------------------------------------------------------------------------------ memory estimators
+def model_to_params(model):
+    """(total parameters, parameters of the largest top-level-leaf layer) of a model."""
+    total = sum(p.numel() for p in model.parameters())
+    largest = max((sum(p.numel() for p in m.parameters(recurse=False)) for m in model.modules()), default=0)
+    return total, largest
+
+
+def estimate_zero2_model_states_mem_needs(total_params, num_gpus_per_node=1, num_nodes=1, cpu_offload=True,
+                                          additional_buffer_factor=1.5):
+    """(host bytes per node, device bytes per GPU) for the model states under ZeRO-2 (reference
+    `stage_1_and_2.py:2396-2420`): 16-bit weights + gradients replicated (4 B / param), fp32 master + Adam moments
+    (16 B / param... 12 B of optimizer state + 4 B fp32 gradient) split over all GPUs or kept on the host."""
+    total_gpus = num_nodes * num_gpus_per_node
+    if cpu_offload:
+        gpu_mem = 2 * total_params
+        cpu_mem = total_params * max(4 * total_gpus, 16) * additional_buffer_factor
+    else:
+        gpu_mem = 4 * total_params + int(16 * total_params / total_gpus)
+        cpu_mem = total_params * 4 * num_gpus_per_node * additional_buffer_factor
+    return int(cpu_mem), int(gpu_mem)
+
+
+def estimate_zero3_model_states_mem_needs(total_params, largest_layer_params, num_gpus_per_node=1, num_nodes=1,
+                                          cpu_offload=True, cpu_offload_params=True, zero_init=True,
+                                          additional_buffer_factor=1.5):
+    """(host bytes per node, device bytes per GPU, bytes of the largest layer) under ZeRO-3 (reference
+    `stage3.py:2613-2660`): everything is split over the GPUs (18 B / param) unless offloaded; the largest layer
+    must be resident gathered (4 B / param: weights + gradients)."""
+    total_gpus = num_nodes * num_gpus_per_node
+    gpus_factor = 1 / num_nodes
+    largest_layer_memory = 4 * largest_layer_params
+    if cpu_offload:
+        if cpu_offload_params:
+            gpu_mem = largest_layer_memory
+            per = 18
+        else:
+            gpu_mem = largest_layer_memory + int(2 * total_params / total_gpus)
+            per = 16
+        cpu_mem = total_params * per * gpus_factor * additional_buffer_factor if zero_init else \
+            total_params * max(4 * num_gpus_per_node, per * gpus_factor) * additional_buffer_factor
+    else:
+        gpu_mem = largest_layer_memory + int(18 * total_params / total_gpus)
+        cpu_mem = (largest_layer_params if zero_init else total_params) * 4 * num_gpus_per_node * \
+            additional_buffer_factor
+    return int(cpu_mem), int(gpu_mem), largest_layer_memory
+
+
+def _gb(n):
+    return f"{n / 2**30:7.2f}GB"
+
+
+def estimate_zero2_model_states_mem_needs_all_cold(total_params, num_gpus_per_node=1, num_nodes=1,
+                                                   additional_buffer_factor=1.5):
+    """Print the ZeRO-2 table (offload on / off) for a parameter count; returns the rows."""
+    rows = []
+    print(f"Estimated memory needed for params, optim states and gradients for a:\nHW: Setup with {num_nodes} "
+          f"node{'s' if num_nodes > 1 else ''}, {num_gpus_per_node} GPU{'s' if num_gpus_per_node > 1 else ''} per "
+          f"node.\nSW: Model with {int(total_params / 1e6)}M total params.\n  per CPU  |  per GPU |   Options")
+    for off in (True, False):
+        cpu, gpu = estimate_zero2_model_states_mem_needs(total_params, num_gpus_per_node, num_nodes, off,
+                                                         additional_buffer_factor)
+        rows.append({"offload_optimizer": off, "cpu": cpu, "gpu": gpu})
+        print(f" {_gb(cpu)} | {_gb(gpu)} | offload_optimizer={'cpu' if off else 'none'}")
+    return rows
+
+
+def estimate_zero2_model_states_mem_needs_all_live(model, num_gpus_per_node=1, num_nodes=1,
+                                                   additional_buffer_factor=1.5):
+    return estimate_zero2_model_states_mem_needs_all_cold(model_to_params(model)[0], num_gpus_per_node, num_nodes,
+                                                          additional_buffer_factor)
+
+
+def estimate_zero3_model_states_mem_needs_all_cold(total_params, largest_layer_params, num_gpus_per_node=1,
+                                                   num_nodes=1, additional_buffer_factor=1.5):
+    rows = []
+    print(f"Estimated memory needed for params, optim states and gradients for a:\nHW: Setup with {num_nodes} "
+          f"node{'s' if num_nodes > 1 else ''}, {num_gpus_per_node} GPU{'s' if num_gpus_per_node > 1 else ''} per "
+          f"node.\nSW: Model with {int(total_params / 1e6)}M total params, {int(largest_layer_params / 1e6)}M "
+          f"largest layer params.\n  per CPU  |  per GPU |   Options")
+    for off_p, off_o in ((True, True), (False, True), (False, False)):
+        for zi in (True, False):
+            cpu, gpu, _ = estimate_zero3_model_states_mem_needs(total_params, largest_layer_params,
+                                                                num_gpus_per_node, num_nodes, off_o, off_p, zi,
+                                                                additional_buffer_factor)
+            rows.append({"offload_param": off_p, "offload_optimizer": off_o, "zero_init": zi, "cpu": cpu,
+                         "gpu": gpu})
+            print(f" {_gb(cpu)} | {_gb(gpu)} | offload_param={'cpu' if off_p else 'none'}, offload_optimizer="
+                  f"{'cpu' if off_o else 'none'}, zero_init={int(zi)}")
+    return rows
+
+
+def estimate_zero3_model_states_mem_needs_all_live(model, num_gpus_per_node=1, num_nodes=1,
+                                                   additional_buffer_factor=1.5):
+    total, largest = model_to_params(model)
+    return estimate_zero3_model_states_mem_needs_all_cold(total, largest, num_gpus_per_node, num_nodes,
+                                                          additional_buffer_factor)
+

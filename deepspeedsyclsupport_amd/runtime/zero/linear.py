@@ -36,3 +36,18 @@ def install_zero3_linear(module: nn.Module):
             m._ds_zero3_linear = True
             n += 1
     return n
+
+
+class LinearModuleForZeroStage3(nn.Linear):
+    """nn.Linear whose autograd function saves the Parameter object, not the gathered weight (reference
+    `runtime/zero/linear.py:113`): under ZeRO-3 the released weight is not kept alive until backward."""
+
+    def forward(self, input):
+        return zero3_linear_wrap(input, self.weight, self.bias)
+
+
+def print_rank_0(message, debug=False, force=False):
+    from ... import comm as dist
+    if (debug or force) and (not dist.is_initialized() or dist.get_rank() == 0):
+        print(message)
+

@@ -19,6 +19,8 @@ embeddings, shared projections). Under ZeRO-3 the fetch hooks of `module` then g
 """
 import functools
 
+from enum import Enum
+
 import torch
 import torch.nn as nn
 
@@ -91,6 +93,86 @@ def register_external_parameter(module, parameter):
 def unregister_external_parameter(module, parameter):
     ext = module.__dict__.get("_ds_external_params", [])
     module.__dict__["_ds_external_params"] = [q for q in ext if q is not parameter]
+
+
+class ZeroParamType(Enum):
+    NORMAL = 1     # partitioned across the data-parallel group
+    PARTITIONED = 2
+    REMOTE = 3     # lives on another device (host / NVMe) until fetched
+
+
+class ZeroParamStatus(Enum):
+    AVAILABLE = 1        # gathered: usable in compute
+    NOT_AVAILABLE = 2    # only this rank's partition is present
+    INFLIGHT = 3         # a gather is in progress
+
+
+class AllGatherHandle:
+    """Completion handle of one parameter gather (reference `partition_parameters.py:620-640`). Gathers here are
+    issued per flat group on the all-gather stream; the handle carries the event compute must wait for."""
+
+    def __init__(self, handle, param, quantization=None):
+        self.handle, self.param, self.quantization = handle, param, quantization
+
+    def wait(self):
+        if self.handle is not None and hasattr(self.handle, "wait"):
+            self.handle.wait()
+        if hasattr(self.param, "ds_status"):
+            self.param.ds_status = ZeroParamStatus.AVAILABLE
+
+
+class AllGatherCoalescedHandle:
+
+    def __init__(self, allgather_handle, params, partitions=None, world_size=1, use_secondary_tensor=False,
+                 forward=False, quantization=None):
+        self.allgather_handle, self.params = allgather_handle, list(params)
+        self.complete = False
+
+    def wait(self):
+        if self.complete:
+            return
+        if self.allgather_handle is not None and hasattr(self.allgather_handle, "wait"):
+            self.allgather_handle.wait()
+        for p in self.params:
+            if hasattr(p, "ds_status"):
+                p.ds_status = ZeroParamStatus.AVAILABLE
+        self.complete = True
+
+
+class NoGatherHandle(AllGatherHandle):
+    """Handle for a single-rank group: nothing to wait for."""
+
+    def __init__(self, param):
+        super().__init__(None, param)
+
+
+class NoGatherCoalescedHandle(AllGatherCoalescedHandle):
+
+    def __init__(self, params):
+        super().__init__(None, params)
+
+
+class MultipleAllGatherHandles:
+
+    def __init__(self, handles):
+        self.handles = list(handles)
+
+    def wait(self):
+        for h in self.handles:
+            h.wait()
+
+
+def free_param(param):
+    """Drop the gathered data of a ZeRO-3 parameter (its partition stays)."""
+    if hasattr(param, "partition"):
+        param.partition()
+    else:
+        param.data = torch.empty(0, dtype=param.dtype, device=param.device)
+
+
+def print_rank_0(message, debug=False, force=False):
+    if (debug or force) and (not dist.is_initialized() or dist.get_rank() == 0):
+        print(message)
 
 
 def is_zero_param(p):

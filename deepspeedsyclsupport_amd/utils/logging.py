@@ -55,3 +55,26 @@ def print_json_dist(message, ranks=None, path=None):
 
 def should_log_le(max_log_level_str):
     return logger.getEffectiveLevel() <= getattr(logging, max_log_level_str.upper())
+
+
+import functools
+
+
+@functools.lru_cache(None)
+def warning_once(*args, **kwargs):
+    """`logger.warning` that fires once per distinct message."""
+    logger.warning(*args, **kwargs)
+
+
+logger.warning_once = warning_once
+
+
+def print_configuration(args, name):
+    logger.info("{}:".format(name))
+    for arg in sorted(vars(args)):
+        logger.info("  {} {} {}".format(arg, "." * (29 - len(arg)), getattr(args, arg)))
+
+
+def get_current_level():
+    return logger.getEffectiveLevel()
+

@@ -58,3 +58,37 @@ def safe_get_local_optimizer_state(param, optim_state_key):
 def safe_get_local_grad(param):
     full = safe_get_full_grad(param)
     return None if full is None else full.reshape(-1)
+
+
+def safe_set_local_fp32_param(param, value):
+    """Overwrite this rank's fragment of the fp32 master (and its 16-bit shard) of `param`; no collective."""
+    opt = _owner(param)
+    if opt is None:
+        param.data.copy_(value.reshape(param.shape))
+    else:
+        opt.set_local_fp32_param(param, value)
+
+
+def safe_set_local_optimizer_state(param, value, optim_state_key):
+    opt = _owner(param)
+    if opt is not None:
+        opt.set_local_optimizer_state(param, value, optim_state_key)
+
+
+# the reference binds these three as methods on each low-precision parameter (`link_hp_params`); as functions they
+# take the parameter first
+def get_full_hp_param(param, optim_state_key=None):
+    return safe_get_full_fp32_param(param) if optim_state_key is None else \
+        safe_get_full_optimizer_state(param, optim_state_key)
+
+
+def set_full_hp_param(param, value, optim_state_key=None):
+    if optim_state_key is None:
+        safe_set_full_fp32_param(param, value)
+    else:
+        safe_set_full_optimizer_state(param, value, optim_state_key)
+
+
+def get_full_hp_grad(param):
+    return safe_get_full_grad(param)
+

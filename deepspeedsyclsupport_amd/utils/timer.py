@@ -197,3 +197,29 @@ class ThroughputTimer:
         if steps > 0 and self.total_elapsed_time > 0:
             return self.batch_size * steps / self.total_elapsed_time
         return float("-inf")
+
+
+class CudaEventTimer:
+    """Elapsed time between two recorded device events (HIP events here), in milliseconds."""
+
+    def __init__(self, start_event, end_event):
+        self.start_event = start_event
+        self.end_event = end_event
+
+    def get_elapsed_msec(self):
+        get_accelerator().current_stream().wait_event(self.end_event)
+        self.end_event.synchronize()
+        return self.start_event.elapsed_time(self.end_event)
+
+
+def trim_mean(data, trim_percent):
+    """Mean of `data` after dropping the `trim_percent` smallest and largest fraction of the values."""
+    assert 0.0 <= trim_percent <= 1.0
+    n = len(data)
+    if n == 0:
+        return 0
+    data = sorted(data)
+    k = int(round(n * trim_percent))
+    kept = data[k:n - k] or data
+    return sum(kept) / len(kept)
+

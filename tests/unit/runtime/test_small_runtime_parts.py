@@ -148,3 +148,55 @@ def _ccl_backend():
 
 def test_ccl_backend_object():
     run_distributed(_ccl_backend, 2)
+
+
+def test_memory_estimators_and_runtime_helpers(capsys):
+    from deepspeedsyclsupport_amd.runtime import utils as U
+    from deepspeedsyclsupport_amd.runtime.zero.stage3 import (estimate_zero3_model_states_mem_needs,
+                                                           estimate_zero3_model_states_mem_needs_all_live)
+    from deepspeedsyclsupport_amd.runtime.zero.stage_1_and_2 import estimate_zero2_model_states_mem_needs
+    P, L = 10**9, 10**8
+    cpu, gpu = estimate_zero2_model_states_mem_needs(P, 8, 1, cpu_offload=False)
+    assert gpu == 4 * P + 16 * P // 8
+    cpu, gpu, big = estimate_zero3_model_states_mem_needs(P, L, 8, 2, cpu_offload=False)
+    assert gpu == 4 * L + 18 * P // 16 and big == 4 * L
+    cpu, gpu, _ = estimate_zero3_model_states_mem_needs(P, L, 8, 1, cpu_offload=True, cpu_offload_params=True)
+    assert gpu == 4 * L and cpu == int(P * 18 * 1.5)
+    rows = estimate_zero3_model_states_mem_needs_all_live(torch.nn.Linear(100, 100), 2, 1)
+    assert len(rows) == 6 and "largest layer params" in capsys.readouterr().out
+    ts = [torch.full((4, ), 3.0), torch.full((9, ), 2.0)]
+    before = U.clip_tensors_by_global_norm(ts, 1.0)
+    assert abs(float(before) - 72**0.5) < 1e-4 and abs(float(U.get_global_norm_of_tensors(ts)) - 1.0) < 1e-4
+    assert U.get_global_norm([3, 4]) == 5.0 and U.prefix_sum_inc([1, 2, 3]) == [1, 3, 6]
+    moved = U.copy_to_device({"a": [ts[0]], "b": 1}, "cpu")
+    assert moved["a"][0] is not ts[0] and torch.equal(moved["a"][0], ts[0]) and moved["b"] == 1
+
+
+def _local_fragments():
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd.utils.tensor_fragment import (safe_get_full_fp32_param,
+                                                               safe_get_local_fp32_param,
+                                                               safe_get_local_optimizer_state,
+                                                               safe_set_local_fp32_param,
+                                                               safe_set_local_optimizer_state)
+    from unit.simple_model import base_config, random_tokens, tiny_llama
+    eng, _, _, _ = ds.initialize(model=tiny_llama(), config=base_config(stage=3, lr=1e-2, mb=2))
+    x = random_tokens(1, 2, 16, seed=1)[0]
+    eng.backward(eng(x, labels=x))
+    eng.step()
+    p = next(q for n, q in eng.module.named_parameters() if "q_proj" in n or "qkv" in n)
+    local = safe_get_local_fp32_param(p)           # None on a rank whose partition holds nothing of p
+    if local is not None:
+        safe_set_local_fp32_param(p, torch.full_like(local, 0.25))
+    full = safe_get_full_fp32_param(p)
+    assert torch.all(full == 0.25)                 # every owning rank wrote its own fragment
+    m = safe_get_local_optimizer_state(p, "exp_avg")
+    if m is not None:
+        safe_set_local_optimizer_state(p, torch.ones_like(m), "exp_avg")
+        assert torch.all(safe_get_local_optimizer_state(p, "exp_avg") == 1)
+        with pytest.raises(ValueError):
+            safe_set_local_fp32_param(p, torch.zeros(local.numel() + 1))
+
+
+def test_local_fragment_setters_zero3():
+    run_distributed(_local_fragments, 2)
