@@ -21,7 +21,11 @@ PATHS = {
     "runtime.zero.stage_1_and_2": [("runtime.zero.flat_optimizer", {"DeepSpeedZeroOptimizer": "DeepSpeedZeroOptimizer",
                                                                    "estimate_zero2_model_states_mem_needs": "estimate_zero2_model_states_mem_needs", "estimate_zero2_model_states_mem_needs_all_live": "estimate_zero2_model_states_mem_needs_all_live", "estimate_zero2_model_states_mem_needs_all_cold": "estimate_zero2_model_states_mem_needs_all_cold", "model_to_params": "model_to_params"})],
     "runtime.zero.partitioned_param_coordinator": [("runtime.zero.coordinator",
-                                                    {"PartitionedParameterCoordinator": "ParamCoordinator"})],
+                                                    {"PartitionedParameterCoordinator": "ParamCoordinator",
+                                                     "ZeRoTraceMode": "ZeRoTraceMode",
+                                                     "InflightParamRegistry": "InflightParamRegistry",
+                                                     "iter_params": "iter_params",
+                                                     "get_all_parameters": "get_all_parameters"})],
     "runtime.zero.parameter_offload": [("runtime.zero.coordinator", {"DeepSpeedZeRoOffload": "ParamCoordinator"})],
     "runtime.zero.mics": [("runtime.zero", {"MiCS_Init": "MiCS_Init", "MiCS_Optimizer": "MiCS_Optimizer"})],
     "runtime.bf16_optimizer": [("runtime.zero.flat_optimizer", {"BF16_Optimizer": "BF16_Optimizer"})],

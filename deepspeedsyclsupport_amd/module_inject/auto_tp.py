@@ -210,3 +210,46 @@ class AutoTP:
                 v = getattr(m, a, None)
                 if isinstance(v, int) and v % self.tp == 0:
                     setattr(m, a, v // self.tp)
+
+
+def __getattr__(name):
+    # `ReplaceWithTensorSlicing` is defined next to the whole-model replacement (replace_module.py imports this file)
+    if name == "ReplaceWithTensorSlicing":
+        from .replace_module import ReplaceWithTensorSlicing
+        return ReplaceWithTensorSlicing
+    raise AttributeError(name)
+
+
+class Loading:
+    """Which layer types are filled from a checkpoint's state dict while sharding a meta-device model (reference
+    `auto_tp.py:124-183`)."""
+
+    @staticmethod
+    def is_load_module(module):
+        names = ("LayerNorm", "Linear", "Embedding", "RMSNorm", "LPLayerNorm", "SharedEmbedding", "OPTLearnedPositionalEmbedding")
+        return isinstance(module, (nn.Linear, nn.Embedding, nn.LayerNorm)) or \
+            any(n.lower() in type(module).__name__.lower() for n in names)
+
+    @staticmethod
+    def load_buffer(module, state_dict, prefix):
+        for name, buf in module.named_buffers(recurse=False):
+            key = prefix + name
+            if key in state_dict:
+                src = state_dict[key]
+                module._buffers[name] = src.to(buf.device if buf.device.type != "meta" else src.device)
+
+    @staticmethod
+    def load(module, state_dict, prefix, mp_group=None):
+        """Fill `module`'s own parameters from `state_dict[prefix + name]`, materialising meta parameters."""
+        for name, p in list(module.named_parameters(recurse=False)):
+            key = prefix + name
+            if key not in state_dict:
+                continue
+            src = state_dict[key]
+            if p.device.type == "meta" or p.shape != src.shape:
+                setattr(module, name, nn.Parameter(src.detach().clone(), requires_grad=p.requires_grad))
+            else:
+                with torch.no_grad():
+                    p.copy_(src)
+        Loading.load_buffer(module, state_dict, prefix)
+

@@ -5,6 +5,8 @@ Instead of swapping each HF layer for a fused CUDA module, injection converts th
 `DSInferenceModel` (one implementation parametrised by the architecture spec); see
 `inference/model_implementations/convert.py` for the per-architecture policies.
 """
+import re
+
 import torch
 
 from ..inference.model_implementations import convert
@@ -107,3 +109,87 @@ def generic_injection(module, dtype=None, enable_cuda_graph=True):
     from .diffusers import inject_pipeline
     inject_pipeline(module, dtype=dtype, enable_cuda_graph=enable_cuda_graph)
     return module
+
+
+class GroupQuantizer:
+    """Symmetric group-wise int8 quantiser of weight matrices (reference `replace_module.py:43-83`): returns the
+    int8 tensor with a `.scale` attribute holding 1 / step per group, laid out for a tensor-parallel split in
+    `count` pieces along `parallel_dim` (each piece gets its own groups, so shards can be cut without
+    re-quantising)."""
+
+    def __init__(self, q_int8=True, group_size=1, num_bits=8, num_groups=0):
+        self.group_size = group_size
+        self.num_bits = num_bits
+        self.q_int8 = q_int8
+        self.num_groups = num_groups
+
+    def quantize(self, inputs, qkv=True, count=1, parallel_dim=0):
+        if not self.q_int8 or not qkv:
+            inputs = torch.nn.Parameter(inputs, requires_grad=False)
+            inputs.scale = torch.empty(1)
+            return inputs
+        q_range = 2**self.num_bits
+        num_groups = self.num_groups if self.num_groups > 0 else inputs.shape[0] // self.group_size
+        x = inputs.to(torch.float32)
+        grouped = x.reshape(num_groups, -1)
+        step = (2 * grouped.abs().amax(dim=1, keepdim=True)).clamp_min(1e-12) / q_range
+        q = (grouped / step).round().clamp(-q_range // 2, q_range // 2 - 1).to(torch.int8).reshape(inputs.shape)
+        out = torch.nn.Parameter(q, requires_grad=False)
+        # per-piece scales: quantise each tensor-parallel piece by its own groups, stacked piece-major
+        scales = []
+        for piece in x.chunk(max(count, 1), dim=parallel_dim):
+            g = piece.reshape(num_groups, -1) if piece.numel() % num_groups == 0 else piece.reshape(1, -1)
+            scales.append((q_range / (2 * g.abs().amax(dim=1)).clamp_min(1e-12)))
+        out.scale = torch.cat([s.reshape(-1) for s in scales]).unsqueeze(0)
+        return out
+
+
+def get_transformer_name(replaced_module):
+    """Qualified name of the ModuleList that holds the model's transformer layers."""
+    best = ""
+    for name, child in replaced_module.named_modules():
+        if isinstance(child, torch.nn.ModuleList) and len(child) > 0 and \
+                sum(1 for _ in child[0].modules()) > 2 and (not best or len(child) >= 1):
+            best = best or name
+    return best
+
+
+def skip_level_0_prefix(model, state_dict):
+    """Models whose checkpoints carry no top-level prefix (BLOOM / OPT style) are loaded from level 1 down."""
+    key = re.search(r": (.*?)Model", str(type(model)))
+    if key is None:
+        key = re.search(r": (.*?)Stack", str(type(model)))
+    if key is None:
+        key = re.match(r"(.*?)Model", type(model).__name__)
+    return key is not None and key.group(1).split(".")[-1].lower() in ("bloom", "opt")
+
+
+def replace_module(model, orig_class, replace_fn, _replace_policy=None, checkpoint=None):
+    """Swap every instance of `orig_class` (a class, or None to use each policy's `_orig_layer_class`) for
+    `replace_fn(child, policy_class, layer_id)` (reference `replace_module.py:586-627`). `_replace_policy` narrows the
+    policies tried to one class. Returns the model."""
+    from .containers import replace_policies
+    policies = [_replace_policy] if _replace_policy is not None else list(replace_policies)
+    targets = {}
+    if orig_class is not None:
+        targets[orig_class] = policies[0] if _replace_policy is not None else None
+    else:
+        for pol in policies:
+            cls = getattr(pol, "_orig_layer_class", None)  # (set by the policy the first time it is constructed)
+            for c in (cls if isinstance(cls, (list, tuple)) else [cls]):
+                if c is not None:
+                    targets[c] = pol
+    layer_id = 0
+    for name, child in list(model.named_modules()):
+        if not name:
+            continue
+        pol = next((p for c, p in targets.items() if isinstance(child, c)), "none")
+        if pol == "none":
+            continue
+        new = replace_fn(child, pol, layer_id)
+        parent_name, _, leaf = name.rpartition(".")
+        parent = model.get_submodule(parent_name) if parent_name else model
+        setattr(parent, leaf, new)
+        layer_id += 1
+    return model
+

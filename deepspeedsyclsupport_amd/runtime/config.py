@@ -39,6 +39,13 @@ ADAM_W_MODE = "adam_w_mode"
 MAX_GRAD_NORM = "max_grad_norm"
 
 
+class ValidationMode:
+    """How checkpoint tag mismatches across ranks are treated (`checkpoint.tag_validation`)."""
+    WARN = "WARN"
+    IGNORE = "IGNORE"
+    FAIL = "FAIL"
+
+
 class DeepSpeedConfigError(Exception):
     pass
 

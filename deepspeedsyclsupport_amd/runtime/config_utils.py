@@ -68,3 +68,33 @@ class ScientificNotationEncoder(json.JSONEncoder):
 
     def iterencode(self, o, _one_shot=False):
         yield self.encode(o)
+
+
+def get_config_default(config, field_name):
+    """Default of a field of a config model class (it must have one)."""
+    field = config.model_fields[field_name]
+    assert not field.is_required(), f"'{field_name}' is a required field and does not have a default value"
+    return field.get_default(call_default_factory=True)
+
+
+class pp_int(int):
+    """An int that prints with thousands separators (or as a custom string) in config dumps."""
+
+    def __new__(cls, val, custom_print_str=None):
+        inst = super().__new__(cls, val)
+        inst.custom_print_str = custom_print_str
+        return inst
+
+    def __repr__(self):
+        return self.custom_print_str if self.custom_print_str else f"{self.real:,}"
+
+
+class DeepSpeedConfigObject:
+    """Base of the plain (non-pydantic) config holders: printable as JSON."""
+
+    def repr(self):
+        return self.__dict__
+
+    def __repr__(self):
+        return json.dumps(self.__dict__, sort_keys=True, indent=4, cls=ScientificNotationEncoder)
+

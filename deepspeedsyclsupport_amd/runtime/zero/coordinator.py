@@ -317,3 +317,33 @@ class ParamCoordinator:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+class ZeRoTraceMode:
+    """States of the module-order trace that drives prefetching (reference
+    `partitioned_param_coordinator.py:38`): RECORD on the first step (and again whenever the order changes),
+    COMPLETE once a step replayed the recorded order, INVALID when a mismatch disabled prefetching."""
+    RECORD = 1
+    COMPLETE = 2
+    INVALID = 3
+
+
+class InflightParamRegistry(dict):
+    """param -> pending gather handle; a parameter may have at most one gather in flight."""
+
+    def __setitem__(self, param, handle):
+        if param in self:
+            raise RuntimeError(f"{getattr(param, 'ds_id', id(param))} already in registry")
+        super().__setitem__(param, handle)
+
+
+def iter_params(module, recurse=False):
+    return (p for _, p in module.named_parameters(recurse=recurse))
+
+
+def get_all_parameters(sub_module, recurse=False):
+    """Own parameters plus registered external ones (`register_external_parameter`)."""
+    import itertools
+    ext = getattr(sub_module, "_external_params", {})
+    return itertools.chain(sub_module.named_parameters(recurse=recurse), ext.items())
+

@@ -50,3 +50,35 @@ def trace_digest(trace):
     """64-bit digest of a fetch trace (list of group ids) for cheap cross-rank comparison."""
     h = hashlib.sha1(",".join(map(str, trace)).encode()).digest()
     return [len(trace), int.from_bytes(h[:7], "little")]
+
+
+def _zero_supported_optimizers():
+    import torch
+    from ...ops.adagrad.cpu_adagrad import DeepSpeedCPUAdagrad
+    from ...ops.adam.cpu_adam import DeepSpeedCPUAdam
+    from ...ops.adam.fused_adam import FusedAdam
+    out = [torch.optim.Adam, torch.optim.AdamW, FusedAdam, DeepSpeedCPUAdam, torch.optim.Adagrad,
+           DeepSpeedCPUAdagrad]
+    try:
+        from ...ops.lion.fused_lion import FusedLion
+        from ...ops.lion.cpu_lion import DeepSpeedCPULion
+        out += [FusedLion, DeepSpeedCPULion]
+    except ImportError:
+        pass
+    return out
+
+
+def is_zero_supported_optimizer(optimizer):
+    """Is the optimizer one of those tested under ZeRO? (others need `zero_allow_untested_optimizer`)"""
+    return type(optimizer) in _zero_supported_optimizers()
+
+
+def get_lst_from_rank0(lst):
+    """Broadcast a list of ints from rank 0; every rank gets rank 0's values."""
+    import torch
+    from ... import comm as dist
+    t = torch.tensor(lst if dist.get_rank() == 0 else [-1] * len(lst), dtype=torch.int64,
+                     device=_device_for(None))
+    dist.broadcast(t, src=0)
+    return t.cpu().tolist()
+
