@@ -457,8 +457,8 @@ class DeepSpeedEngine(nn.Module):
             raise NotImplementedError("fp16.fp16_master_weights_and_grads: master weights are kept in fp32 (or as a "
                                       "bf16 weight + 16-bit residual with bf16.split_master_weights)")
         if cfg.mics_hierarchial_params_gather:
-            log_dist("mics_hierarchical_params_gather: MiCS shard groups are laid inside one xGMI node, where a single "
-                     "all-gather already uses every link; the two-level gather is not used", ranks=[0])
+            log_dist("mics_hierarchical_params_gather: used for MiCS shard groups that span several nodes (two-level "
+                     "all-gather); a shard group inside one xGMI node gathers in one step", ranks=[0])
         for key, default in (("round_robin_gradients", False), ("legacy_stage1", False),
                              ("pipeline_loading_checkpoint", False), ("use_multi_rank_bucket_allreduce", True),
                              ("allgather_partitions", True), ("contiguous_gradients", True)):

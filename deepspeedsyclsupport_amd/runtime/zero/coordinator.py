@@ -178,6 +178,9 @@ class ParamCoordinator:
         elif self.qwz or (self.qnt and g.frozen):
             from .zeropp import quantized_all_gather
             quantized_all_gather(g.full, shard, g.dp_group)
+        elif getattr(self.opt, "mics_hier", None) is not None and g.dp_group is self.opt.mics_shard_group:
+            from .zeropp import hierarchical_all_gather
+            hierarchical_all_gather(g.full, shard, *self.opt.mics_hier)
         else:
             dist.all_gather_into_tensor(g.full, shard, group=g.dp_group)
         if hpz is not None and not self.in_backward:

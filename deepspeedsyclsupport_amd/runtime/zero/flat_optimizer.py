@@ -831,6 +831,7 @@ class FlatZeroOptimizer(ZeROOptimizer):
         self.mics_shard_group = None
         self.mics_replica_group = None
         self.mics_replicas = 1
+        self.mics_hier = None
         S = int(getattr(self.zc, "mics_shard_size", -1) or -1) if self.zc is not None else -1
         if S <= 1 or S >= self.dp or self.stage < 1:
             return
@@ -848,6 +849,24 @@ class FlatZeroOptimizer(ZeROOptimizer):
             if me in grp:
                 self.mics_replica_group = g
         self.mics_replicas = self.dp // S
+        # mics_hierarchical_params_gather: a shard group that spans nodes gathers in two levels
+        self.mics_hier = None
+        node = int(os.environ.get("DS_NODE_SIZE", 0)) or max(get_accelerator().device_count(), 1)
+        if bool(getattr(self.zc, "mics_hierarchical_params_gather", False)) and S > node and S % node == 0:
+            intra = inter = None
+            for i in range(self.dp // S):
+                grp = ranks[i * S:(i + 1) * S]
+                for a in range(S // node):            # the ranks of one node inside this shard group
+                    sub = grp[a * node:(a + 1) * node]
+                    g = dist.new_group(sub)
+                    if me in sub:
+                        intra = g
+                for b in range(node):                 # one local index across the shard group's nodes
+                    sub = grp[b::node]
+                    g = dist.new_group(sub)
+                    if me in sub:
+                        inter = g
+            self.mics_hier = (intra, inter)
 
     def _grad_items(self):
         """[(og, moff, n, grad_1d, lp_1d, scale)] covering every DEVICE-resident master element that has a gradient

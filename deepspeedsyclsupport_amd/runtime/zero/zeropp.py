@@ -146,3 +146,23 @@ class HpzState:
     @staticmethod
     def drop(g):
         g.secondary = None
+
+
+@torch.no_grad()
+def hierarchical_all_gather(full, shard, intra_group, inter_group):
+    """full[nodes * local * seg] <- every rank's shard, in rank order (rank = node * local + local index), as two
+    all-gathers (reference `runtime/zero/mics.py:234-300`): first between nodes among the ranks of one local index
+    (each message is a whole shard, all local ranks use the network at once), then inside the node over xGMI with
+    `nodes` shards per message; one strided copy puts the [local, node] result into rank order."""
+    local = dist.get_world_size(intra_group)
+    nodes = dist.get_world_size(inter_group)
+    seg = shard.numel()
+    if full.numel() != nodes * local * seg:
+        raise ValueError(f"output of {full.numel()} elements is not nodes * local * shard = {nodes * local * seg}")
+    across = torch.empty(nodes * seg, dtype=shard.dtype, device=shard.device)
+    dist.all_gather_into_tensor(across, shard.contiguous(), group=inter_group)
+    by_local = torch.empty(local * nodes * seg, dtype=shard.dtype, device=shard.device)
+    dist.all_gather_into_tensor(by_local, across, group=intra_group)
+    full.view(nodes, local, seg).copy_(by_local.view(local, nodes, seg).transpose(0, 1))
+    return full
+

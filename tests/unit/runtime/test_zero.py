@@ -122,14 +122,19 @@ def test_mics(stage, tmp_path):
     assert got == pytest.approx(ref, rel=1e-4, abs=1e-5), (got, ref)
 
 
-def _mics_run(stage, world, out):
+def _mics_run(stage, world, out, hierarchical=False):
+    import os
     import deepspeedsyclsupport_amd as ds
     from deepspeedsyclsupport_amd import comm as dist
     rank = dist.get_rank()
     cfg = base_config(stage=stage, lr=1e-2, mb=2, clip=1.0)
     cfg["zero_optimization"]["mics_shard_size"] = 2
+    if hierarchical:  # pretend every rank is its own node: the shard group of 2 then spans 2 "nodes"
+        os.environ["DS_NODE_SIZE"] = "1"
+        cfg["zero_optimization"]["mics_hierarchical_params_gather"] = True
     eng, _, _, _ = ds.initialize(model=tiny_llama(), config=cfg)
     assert eng.optimizer.mics_replicas == 2 and eng.optimizer.partition_count() == 2
+    assert (eng.optimizer.mics_hier is not None) == hierarchical
     losses = []
     for x in random_tokens(3, 2, 16, seed=100 + rank):
         loss = eng(x, labels=x)
@@ -140,6 +145,33 @@ def _mics_run(stage, world, out):
         losses.append(float(t) / world)
     if rank == 0:
         torch.save({"losses": losses}, out)
+
+
+def test_mics_hierarchical_gather(tmp_path):
+    """`mics_hierarchical_params_gather`: the two-level parameter gather trains exactly like the one-level one."""
+    world = 4
+    out = str(tmp_path / "m.pt")
+    run_distributed(_mics_run, world, 3, world, out, True)
+    got = torch.load(out, weights_only=True)["losses"]
+    ref, _ = _reference_losses(world, 3, 1, 2, 16, 1e-2, 1.0)
+    assert got == pytest.approx(ref, rel=1e-4, abs=1e-5), (got, ref)
+
+
+def _hier_gather_fn():
+    from deepspeedsyclsupport_amd import comm as dist
+    from deepspeedsyclsupport_amd.runtime.zero.zeropp import hierarchical_all_gather
+    rank = dist.get_rank()
+    groups = {}
+    for name, ranks in (("n0", [0, 1]), ("n1", [2, 3]), ("l0", [0, 2]), ("l1", [1, 3])):
+        groups[name] = dist.new_group(ranks)
+    intra, inter = groups[f"n{rank // 2}"], groups[f"l{rank % 2}"]
+    full = torch.empty(4 * 5)
+    hierarchical_all_gather(full, torch.full((5, ), float(rank)), intra, inter)
+    assert full.view(4, 5)[:, 0].tolist() == [0.0, 1.0, 2.0, 3.0]
+
+
+def test_hierarchical_all_gather_rank_order():
+    run_distributed(_hier_gather_fn, 4)
 
 
 def test_tiled_linear_matches_linear():
