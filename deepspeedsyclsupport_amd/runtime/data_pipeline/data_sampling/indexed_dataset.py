@@ -215,15 +215,262 @@ class MMapIndexedDatasetBuilder:
             f.write(np.asarray(self._doc_idx, dtype=np.int64).tobytes(order="C"))
 
 
+# ------------------------------------------------------------------------------------------------ legacy formats
+# "lazy" / "cached": the older Megatron / fairseq index ("TNTIDX" header, big-endian-free struct fields, then the
+# dimension offsets, data offsets, sizes and document index as int64 arrays); the data file is the items back to back.
+_LEGACY_MAGIC = b"TNTIDX\x00\x00"
+
+
+def read_longs(f, n):
+    a = np.empty(n, dtype=np.int64)
+    f.readinto(a)
+    return a
+
+
+def write_longs(f, a):
+    f.write(np.array(a, dtype=np.int64))
+
+
+def create_doc_idx(sizes):
+    """Document boundaries from item sizes: an item of size 0 ends a document."""
+    doc_idx = [0]
+    for i, s in enumerate(sizes):
+        if s == 0:
+            doc_idx.append(i + 1)
+    return doc_idx
+
+
+def exscan_from_cumsum_(arr):
+    """In place: inclusive prefix sum -> exclusive prefix sum (shift right, first element 0)."""
+    if arr.size > 1:
+        arr[1:] = arr[:-1]
+    if arr.size > 0:
+        arr[0] = 0
+
+
+def get_pointers_with_total(sizes, elemsize, dtype):
+    """(byte offset of every item, total bytes) from item sizes in elements."""
+    pointers = np.array(sizes, dtype=dtype)
+    np.cumsum(pointers, axis=0, out=pointers)
+    total = int(pointers[-1]) * elemsize if len(sizes) else 0
+    exscan_from_cumsum_(pointers)
+    pointers *= elemsize
+    return pointers, total
+
+
+class IndexedDataset(torch.utils.data.Dataset):
+    """Reader of the legacy index format; items are read from the data file on access ("lazy")."""
+
+    def __init__(self, path):
+        super().__init__()
+        self.path = path
+        self.data_file = None
+        self.read_index(path)
+
+    def read_index(self, path):
+        import struct
+        with open(index_file_path(path), "rb") as f:
+            magic = f.read(8)
+            assert magic == _LEGACY_MAGIC, "Index file doesn't match expected format. Make sure that --dataset-impl " \
+                "is configured properly."
+            assert struct.unpack("<Q", f.read(8)) == (1, )
+            dcode, self.element_size = struct.unpack("<QQ", f.read(16))
+            self.dtype = DTYPES[dcode]
+            self._len, self.s = struct.unpack("<QQ", f.read(16))
+            self.doc_count = struct.unpack("<Q", f.read(8))[0]
+            self.dim_offsets = read_longs(f, self._len + 1)
+            self.data_offsets = read_longs(f, self._len + 1)
+            self.sizes = read_longs(f, self.s)
+            self.doc_idx = read_longs(f, self.doc_count)
+
+    def read_data(self, path):
+        self.data_file = open(data_file_path(path), "rb", buffering=0)
+
+    def check_index(self, i):
+        if i < 0 or i >= self._len:
+            raise IndexError("index out of range")
+
+    def __del__(self):
+        if self.data_file:
+            self.data_file.close()
+
+    def __getitem__(self, idx):
+        if not self.data_file:
+            self.read_data(self.path)
+        if isinstance(idx, int):
+            self.check_index(idx)
+            shape = self.sizes[self.dim_offsets[idx]:self.dim_offsets[idx + 1]]
+            a = np.empty(shape, dtype=self.dtype)
+            self.data_file.seek(int(self.data_offsets[idx]) * self.element_size)
+            self.data_file.readinto(a)
+            return a
+        if isinstance(idx, slice):
+            start, stop, step = idx.indices(len(self))
+            if step != 1:
+                raise ValueError("Slices into indexed_dataset must be contiguous")
+            sizes = self.sizes[self.dim_offsets[start]:self.dim_offsets[stop]]
+            a = np.empty(int(sum(sizes)), dtype=self.dtype)
+            self.data_file.seek(int(self.data_offsets[start]) * self.element_size)
+            self.data_file.readinto(a)
+            return np.split(a, np.cumsum(sizes)[:-1])
+        raise TypeError(f"unsupported index {idx!r}")
+
+    def __len__(self):
+        return self._len
+
+    def num_tokens(self, index):
+        return self.sizes[index]
+
+    def size(self, index):
+        return self.sizes[index]
+
+    @staticmethod
+    def exists(path):
+        return os.path.exists(index_file_path(path)) and os.path.exists(data_file_path(path))
+
+    @property
+    def supports_prefetch(self):
+        return False
+
+
+class IndexedCachedDataset(IndexedDataset):
+    """Legacy format with `prefetch(indices)`: the requested items are read once into one array and served from
+    it."""
+
+    def __init__(self, path):
+        super().__init__(path)
+        self.cache = None
+        self.cache_index = {}
+
+    @property
+    def supports_prefetch(self):
+        return True
+
+    def prefetch(self, indices):
+        if all(i in self.cache_index for i in indices):
+            return
+        if not self.data_file:
+            self.read_data(self.path)
+        indices = sorted(set(indices))
+        total = sum(int(self.data_offsets[i + 1] - self.data_offsets[i]) for i in indices)
+        self.cache = np.empty(total, dtype=self.dtype)
+        self.cache_index.clear()
+        ptx = 0
+        for i in indices:
+            self.cache_index[i] = ptx
+            size = int(self.data_offsets[i + 1] - self.data_offsets[i])
+            self.data_file.seek(int(self.data_offsets[i]) * self.element_size)
+            self.data_file.readinto(self.cache[ptx:ptx + size])
+            ptx += size
+        if self.data_file:
+            self.data_file.close()
+            self.data_file = None
+
+    def __getitem__(self, idx):
+        if isinstance(idx, int) and idx in self.cache_index:
+            self.check_index(idx)
+            shape = self.sizes[self.dim_offsets[idx]:self.dim_offsets[idx + 1]]
+            ptx = self.cache_index[idx]
+            return self.cache[ptx:ptx + int(np.prod(shape))].reshape(shape).copy()
+        if isinstance(idx, slice):
+            return [self[i] for i in range(*idx.indices(len(self)))]
+        return super().__getitem__(idx)
+
+
+class IndexedDatasetBuilder:
+    """Writer of the legacy format."""
+    element_sizes = {np.uint8: 1, np.int8: 1, np.int16: 2, np.int32: 4, np.int64: 8, np.float64: 8, np.double: 8}
+
+    def __init__(self, out_file, dtype=np.int32):
+        self.out_file = open(out_file, "wb")
+        self.dtype = dtype
+        self.data_offsets, self.dim_offsets, self.sizes, self.doc_idx = [0], [0], [], [0]
+        self.element_size = np.dtype(dtype).itemsize
+
+    def add_item(self, tensor):
+        arr = np.asarray(tensor.numpy() if torch.is_tensor(tensor) else tensor, dtype=self.dtype)
+        n = self.out_file.write(arr.tobytes())
+        self.data_offsets.append(self.data_offsets[-1] + n // self.element_size)
+        self.sizes.extend(arr.shape)
+        self.dim_offsets.append(self.dim_offsets[-1] + arr.ndim)
+
+    def end_document(self):
+        self.doc_idx.append(len(self.sizes))
+
+    def merge_file_(self, another_file):
+        other = IndexedDataset(another_file)
+        assert other.dtype == self.dtype
+        doc_offset = len(self.sizes)
+        begin = self.data_offsets[-1]
+        self.data_offsets.extend(begin + int(o) for o in other.data_offsets[1:])
+        self.sizes.extend(int(x) for x in other.sizes)
+        begin = self.dim_offsets[-1]
+        self.dim_offsets.extend(begin + int(o) for o in other.dim_offsets[1:])
+        self.doc_idx.extend(doc_offset + int(d) for d in other.doc_idx[1:])
+        with open(data_file_path(another_file), "rb") as f:
+            while True:
+                data = f.read(1 << 20)
+                if not data:
+                    break
+                self.out_file.write(data)
+
+    def finalize(self, index_file):
+        import struct
+        self.out_file.close()
+        with open(index_file, "wb") as index:
+            index.write(_LEGACY_MAGIC)
+            index.write(struct.pack("<Q", 1))
+            index.write(struct.pack("<QQ", code(self.dtype), self.element_size))
+            index.write(struct.pack("<QQ", len(self.data_offsets) - 1, len(self.sizes)))
+            index.write(struct.pack("<Q", len(self.doc_idx)))
+            write_longs(index, self.dim_offsets)
+            write_longs(index, self.data_offsets)
+            write_longs(index, self.sizes)
+            write_longs(index, self.doc_idx)
+
+
+# ------------------------------------------------------------------------------------------------ factories
+def get_available_dataset_impl():
+    return ["lazy", "cached", "mmap"]
+
+
+def infer_dataset_impl(path):
+    """"cached" for a legacy index, "mmap" for the memory-mapped one, None when the index is neither / absent."""
+    if not IndexedDataset.exists(path):
+        print(f"Dataset does not exist: {path}")
+        print("Path should be a basename that both .idx and .bin can be appended to get full filenames.")
+        return None
+    with open(index_file_path(path), "rb") as f:
+        magic = f.read(8)
+    if magic == _LEGACY_MAGIC:
+        return "cached"
+    if magic == _HDR_MAGIC[:8]:
+        return "mmap"
+    return None
+
+
+def dataset_exists(path, impl):
+    return MMapIndexedDataset.exists(path) if impl == "mmap" else IndexedDataset.exists(path)
+
+
 def make_builder(out_file, impl="mmap", vocab_size=None, dtype=None):
-    assert impl == "mmap", "only the mmap implementation is provided"
-    return MMapIndexedDatasetBuilder(out_file, dtype=dtype or best_fitting_dtype(vocab_size))
+    if impl == "mmap":
+        return MMapIndexedDatasetBuilder(out_file, dtype=dtype or best_fitting_dtype(vocab_size))
+    return IndexedDatasetBuilder(out_file) if dtype is None else IndexedDatasetBuilder(out_file, dtype=dtype)
 
 
 def make_dataset(path, impl="mmap", skip_warmup=True):
-    if not MMapIndexedDataset.exists(path):
+    if not IndexedDataset.exists(path):
         raise FileNotFoundError(f"dataset {path}.idx/.bin not found")
-    return MMapIndexedDataset(path, skip_warmup)
+    if impl == "infer":
+        impl = infer_dataset_impl(path)
+    if impl == "lazy":
+        return IndexedDataset(path)
+    if impl == "cached":
+        return IndexedCachedDataset(path)
+    if impl == "mmap":
+        return MMapIndexedDataset(path, skip_warmup)
+    raise ValueError(f"Unknown dataset implementation: {impl}")
 
 
 def create_mmap_dataset_builder(fname, dtype):

@@ -200,3 +200,34 @@ def _local_fragments():
 
 def test_local_fragment_setters_zero3():
     run_distributed(_local_fragments, 2)
+
+
+def test_legacy_indexed_dataset_formats(tmp_path):
+    """The pre-mmap index format ("lazy" / "cached" readers, builder, merge) next to the mmap one."""
+    import numpy as np
+
+    from deepspeedsyclsupport_amd.runtime.data_pipeline.data_sampling import indexed_dataset as I
+    base = str(tmp_path / "legacy")
+    items = [np.arange(5), np.arange(3) + 10, np.arange(7) + 100]
+    b = I.make_builder(I.data_file_path(base), impl="cached", dtype=np.int32)
+    for it in items:
+        b.add_item(torch.tensor(it))
+    b.end_document()
+    b.finalize(I.index_file_path(base))
+    assert I.infer_dataset_impl(base) == "cached" and I.dataset_exists(base, "lazy")
+    ds = I.make_dataset(base, "infer")
+    assert isinstance(ds, I.IndexedCachedDataset) and len(ds) == 3 and ds.doc_idx.tolist() == [0, 3]
+    ds.prefetch([0, 2])
+    assert ds[2].tolist() == items[2].tolist() and ds[1].tolist() == items[1].tolist()
+    lazy = I.make_dataset(base, "lazy")
+    assert [x.tolist() for x in lazy[0:2]] == [items[0].tolist(), items[1].tolist()]
+    other = str(tmp_path / "other")
+    b2 = I.IndexedDatasetBuilder(I.data_file_path(other), dtype=np.int32)
+    b2.add_item(torch.tensor([7, 8]))
+    b2.merge_file_(base)
+    b2.finalize(I.index_file_path(other))
+    merged = I.IndexedDataset(other)
+    assert len(merged) == 4 and merged[3].tolist() == items[2].tolist() and merged[0].tolist() == [7, 8]
+    ptr, total = I.get_pointers_with_total([2, 3, 4], 4, np.int64)
+    assert ptr.tolist() == [0, 8, 20] and total == 36 and I.create_doc_idx([3, 0, 2, 0]) == [0, 2, 4]
+    assert I.get_available_dataset_impl() == ["lazy", "cached", "mmap"]
