@@ -36,6 +36,59 @@ def _cmd(args):
         return ""
 
 
+def ninja_installed():
+    try:
+        import ninja  # noqa: F401
+        return True
+    except ImportError:
+        return shutil.which("ninja") is not None
+
+
+def hipcc_version():
+    """Version line of the HIP compiler, or None when hipcc is not installed."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        return None
+    lines = _cmd([hipcc, "--version"]).splitlines()
+    return lines[0] if lines else None
+
+
+nvcc_version = hipcc_version  # the reference's name for "device compiler version"
+
+
+def human_readable_size(size):
+    units = ["B", "KB", "MB", "GB", "TB"]
+    i = 0
+    size = float(size)
+    while size >= 1024 and i < len(units) - 1:
+        size /= 1024
+        i += 1
+    return f"{size:.2f} {units[i]}"
+
+
+def get_shm_size():
+    """(human-readable size of /dev/shm, warning or None): RCCL and the host shm all-reduce need room there."""
+    try:
+        st = os.statvfs("/dev/shm")
+    except OSError as e:
+        return "UNKNOWN", str(e)
+    size = st.f_frsize * st.f_blocks
+    warn = None
+    if size < 512 * 1024**2:
+        warn = (f"/dev/shm is {human_readable_size(size)}: multi-process collectives may fail; under docker pass "
+                f"--shm-size=1g or larger")
+    return human_readable_size(size), warn
+
+
+def parse_arguments():
+    import argparse
+    parser = argparse.ArgumentParser()
+    parser.add_argument("--hide_operator_status", action="store_true",
+                        help="Suppress display of installation and compatibility statuses of DeepSpeed operators.")
+    parser.add_argument("--hide_errors_and_warnings", action="store_true", help="Suppress warning and error messages.")
+    return parser.parse_args()
+
+
 def debug_report():
     from . import __version__
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
@@ -55,6 +108,8 @@ def debug_report():
         ("deepspeedsyclsupport_amd version", __version__),
         ("target arch", os.environ.get("DS_ROCM_ARCH", os.environ.get("PYTORCH_ROCM_ARCH", "gfx950"))),
         ("GPU available", torch.cuda.is_available()),
+        ("ninja", ninja_installed()),
+        ("shared memory (/dev/shm) size", get_shm_size()[0]),
     ]
     if torch.cuda.is_available():
         p = torch.cuda.get_device_properties(0)

@@ -211,3 +211,27 @@ if __name__ == "__main__":
     a = ap.parse_args()
     convert_zero_checkpoint_to_fp32_state_dict(a.checkpoint_dir, a.output_file, a.tag, a.exclude_frozen_parameters,
                                                a.safe_serialization)
+
+
+# ---- file discovery helpers with the reference's names
+def atoi(text):
+    return int(text) if text.isdigit() else text
+
+
+def natural_keys(text):
+    """Sort key that orders "rank_2" before "rank_10"."""
+    import re
+    return [atoi(c) for c in re.split(r"(\d+)", text)]
+
+
+def get_checkpoint_files(checkpoint_dir, glob_pattern):
+    import glob
+    files = sorted(glob.glob(os.path.join(checkpoint_dir, glob_pattern)), key=natural_keys)
+    if not files:
+        raise FileNotFoundError(f"can't find {glob_pattern} files in directory '{checkpoint_dir}'")
+    return files
+
+
+def get_model_state_files(checkpoint_dir):
+    return get_checkpoint_files(checkpoint_dir, "*_model_states.pt")
+
