@@ -135,7 +135,8 @@ PATHS = {
         ("ops.transformer.inference.layer", {"DeepSpeedOPTInference": "DeepSpeedTransformerInference"})],
     # ---- inference v2: the reference's one-class-per-file tree over this package's per-family modules
     "inference.v2.ragged.blocked_allocator": [("inference.kv_cache", {"BlockedAllocator": "BlockedAllocator"})],
-    "inference.v2.ragged.kv_cache": [("inference.kv_cache", {"BlockedKVCache": "BlockedKVCache"})],
+    "inference.v2.ragged.kv_cache": [("inference.kv_cache", {"BlockedKVCache": "BlockedKVCache",
+                                                             "split_kv": "split_kv"})],
     "inference.v2.ragged.manager_configs": [("inference.v2.config_v2", "*")],
     **{f"inference.v2.kernels.core_ops.{d}.{f}": [("inference.v2.kernels.core_ops", {n: n for n in names})]
        for d, f, names in (

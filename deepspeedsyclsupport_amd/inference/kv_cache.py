@@ -54,6 +54,56 @@ class BlockedKVCache:
     def bytes(self):
         return 2 * sum(t.numel() * t.element_size() for t in self.k)
 
+    # ---- the reference's cache-object interface (`inference/v2/ragged/kv_cache.py:40-208`)
+    @property
+    def num_caches(self):
+        """Cache groups (models with several attention geometries would hold one each): one here."""
+        return 1
+
+    @property
+    def free_blocks(self):
+        return torch.tensor([self.allocator.free_blocks], dtype=torch.int32)
+
+    def reserve(self, num_blocks, cache_group=0):
+        """Take `num_blocks` block ids out of the free list."""
+        return torch.tensor(self.allocator.allocate(int(num_blocks)), dtype=torch.int32)
+
+    def free(self, blocks, cache_group=0):
+        self.allocator.free(blocks.tolist() if torch.is_tensor(blocks) else blocks)
+
+    def get_cache(self, cache_id, cache_group=0):
+        """(keys, values) of layer `cache_id`, each [blocks, kv_heads, block_size, head_dim]."""
+        return self.k[cache_id], self.v[cache_id]
+
+    def offload(self, blocks, cache_group=0):
+        """Copy the given blocks of every layer to pinned host memory (the blocks stay allocated); returns the
+        handle `restore` takes."""
+        idx = torch.as_tensor(blocks, dtype=torch.long, device=self.k[0].device)
+        pin = torch.device(self.device).type == "cuda" if self.device is not None else False
+        host = []
+        for k, v in zip(self.k, self.v):
+            hk = torch.empty((idx.numel(), ) + tuple(k.shape[1:]), dtype=k.dtype, pin_memory=pin)
+            hv = torch.empty_like(hk, pin_memory=pin)
+            hk.copy_(k.index_select(0, idx), non_blocking=pin)
+            hv.copy_(v.index_select(0, idx), non_blocking=pin)
+            host.append((hk, hv))
+        if pin:
+            torch.cuda.current_stream().synchronize()
+        return {"blocks": idx.cpu(), "data": host}
+
+    def restore(self, handle, blocks=None, cache_group=0):
+        """Write offloaded blocks back, to their old ids or to `blocks` (same count)."""
+        idx = torch.as_tensor(handle["blocks"] if blocks is None else blocks, dtype=torch.long,
+                              device=self.k[0].device)
+        for (hk, hv), k, v in zip(handle["data"], self.k, self.v):
+            k.index_copy_(0, idx, hk.to(k.device, non_blocking=True))
+            v.index_copy_(0, idx, hv.to(v.device, non_blocking=True))
+
+
+def split_kv(kv_cache):
+    """(keys, values) of a stacked [2, ...] cache tensor or an already split pair."""
+    return kv_cache[0], kv_cache[1]
+
 
 class SequenceState:
     """Per-sequence bookkeeping: tokens already in cache and owned block ids."""

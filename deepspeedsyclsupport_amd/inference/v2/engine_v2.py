@@ -41,6 +41,7 @@ class InferenceEngineV2:
             num_blocks = BlockedKVCache.blocks_for_memory(avail, spec.num_layers, hk, bs, spec.head_dim, model.dtype)
         model.allocate_cache(num_blocks, bs)
         self._state_manager = DSStateManager(sm, num_blocks, bs)
+        self._state_manager.attach_cache(getattr(model, "cache", None))
         self._device = model.device if model.device is not None else torch.device("cpu")
         self._batch = RaggedBatchWrapper(sm, bs, self._device)
 

@@ -12,6 +12,7 @@ class DSStateManager:
         self.block_size = block_size
         self.allocator = BlockedAllocator(num_blocks)
         self._seqs = {}
+        self._kv_cache = None
 
     @property
     def n_tracked_sequences(self):
@@ -24,6 +25,29 @@ class DSStateManager:
     @property
     def free_blocks(self):
         return self.allocator.free_blocks
+
+    @property
+    def kv_block_size(self):
+        return self.block_size
+
+    @property
+    def n_kv_cache_groups(self):
+        return 1
+
+    def attach_cache(self, kv_cache):
+        """The model's `BlockedKVCache` (set by the engine once the model has allocated it)."""
+        self._kv_cache = kv_cache
+        if kv_cache is not None and getattr(kv_cache, "allocator", None) is not None \
+                and kv_cache.allocator.num_blocks == self.allocator.num_blocks:
+            self.allocator = kv_cache.allocator   # one free list for `cache.reserve / free` and the manager
+
+    def get_cache(self, cache_id, cache_group=0):
+        """(keys, values) of layer `cache_id`."""
+        return self._kv_cache.get_cache(cache_id, cache_group)
+
+    def query(self, uid=None):
+        """The tracked sequence `uid`, or None."""
+        return self._seqs.get(uid)
 
     def get_sequence(self, uid):
         return self._seqs.get(uid)

@@ -41,6 +41,20 @@ class DSSequenceDescriptor(BaseSequenceDescriptor):
     def cur_allocated_blocks(self):
         return len(self.blocks)
 
+    @property
+    def max_context(self):
+        """Tokens the blocks owned so far can hold."""
+        return len(self.blocks) * self.block_size
+
+    @property
+    def all_block_ids(self):
+        return list(self.blocks)
+
+    def free_kv_cache(self, free_ids, cache_group=0):
+        """Forget blocks handed back to the allocator (sliding-window models release the oldest ones)."""
+        drop = {int(i) for i in free_ids}
+        self.blocks = [b for b in self.blocks if b not in drop]
+
     def kv_cache_ids(self, cache_group=0, on_device=False):
         return self.blocks
 

@@ -703,6 +703,149 @@ class DeepSpeedEngine(nn.Module):
         """Kept for API parity: reduction already happened in `backward` (bucketed on the comm stream)."""
         return
 
+    # ---- explicit gradient reductions over module `.grad`s (reference `engine.py:2326-2518`). The engine's own
+    # path reduces inside the flat-group optimizer; these serve code that drives the reduction itself (custom
+    # loops, engines built without an optimizer).
+    def allreduce_bucket(self, bucket, dp_group=None, dp_world_size=None):
+        """All-reduce a list of same-dtype dense tensors as ONE flat buffer; returns the averaged flat tensor."""
+        from torch._utils import _flatten_dense_tensors
+        group = dp_group if dp_group is not None else self.seq_data_parallel_group
+        world = dp_world_size or dist.get_world_size(group)
+        flat = _flatten_dense_tensors(bucket)
+        comm_dtype = getattr(self, "communication_data_type", None)
+        comm_dtype = comm_dtype() if callable(comm_dtype) else comm_dtype
+        send = flat.to(comm_dtype) if comm_dtype is not None and comm_dtype != flat.dtype else flat
+        pre = float(self._config.gradient_predivide_factor or 1.0) if not self._config.prescale_gradients else world
+        if pre != 1.0:
+            send.mul_(1.0 / pre)
+        dist.all_reduce(send, group=group)
+        post = world / pre
+        if post != 1.0:
+            send.mul_(1.0 / post)
+        if send is not flat:
+            flat.copy_(send)
+        return flat
+
+    def allreduce_and_copy(self, small_bucket, dp_group=None, dp_world_size=None):
+        from torch._utils import _unflatten_dense_tensors
+        flat = self.allreduce_bucket(small_bucket, dp_group, dp_world_size)
+        for buf, synced in zip(small_bucket, _unflatten_dense_tensors(flat, small_bucket)):
+            buf.copy_(synced)
+
+    def allreduce_no_retain(self, bucket, dp_group=None, numel_per_bucket=500000000, dp_world_size=None):
+        small, numel = [], 0
+        for t in bucket:
+            small.append(t)
+            numel += t.numel()
+            if numel > numel_per_bucket:
+                self.allreduce_and_copy(small, dp_group, dp_world_size)
+                small, numel = [], 0
+        if small:
+            self.allreduce_and_copy(small, dp_group, dp_world_size)
+
+    def sparse_all_gather(self, value, dp_group=None):
+        """Concatenation of every rank's rows of a 1-D / 2-D tensor whose leading size differs per rank."""
+        group = dp_group if dp_group is not None else self.seq_data_parallel_group
+        world = dist.get_world_size(group)
+        sizes = self.all_gather_scalar(value.shape[0], group)
+        width = max(sizes)
+        pad = torch.zeros((width, ) + tuple(value.shape[1:]), dtype=value.dtype, device=value.device)
+        pad[:value.shape[0]].copy_(value)
+        out = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(out, pad, group=group)
+        return [o[:n] for o, n in zip(out, sizes)]
+
+    def all_gather_scalar(self, value, dp_group=None):
+        group = dp_group if dp_group is not None else self.seq_data_parallel_group
+        world = dist.get_world_size(group)
+        dev = self.device if dist.get_backend(group) != "gloo" else "cpu"
+        t = torch.tensor([int(value)], dtype=torch.long, device=dev)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t, group=group)
+        return [int(o.item()) for o in out]
+
+    def sparse_allreduce(self, sparse, dp_group=None, dp_world_size=None):
+        """Average a `SparseTensor` across ranks: indices and rows of every rank concatenated, rows divided by the
+        group size (duplicates add up when the tensor is made dense)."""
+        group = dp_group if dp_group is not None else self.seq_data_parallel_group
+        world = dp_world_size or dist.get_world_size(group)
+        sparse.values = sparse.values / world
+        sparse.indices = torch.cat(self.sparse_all_gather(sparse.indices, group))
+        sparse.values = torch.cat(self.sparse_all_gather(sparse.values, group))
+        return sparse
+
+    def sparse_allreduce_bucket(self, bucket, dp_group=None, dp_world_size=None):
+        return [self.sparse_allreduce(s, dp_group, dp_world_size) for s in bucket]
+
+    def sparse_allreduce_no_retain(self, bucket, dp_group=None, dp_world_size=None):
+        for s in self.sparse_allreduce_bucket(bucket, dp_group, dp_world_size):
+            if s.orig_dense_tensor is not None:
+                s.orig_dense_tensor.data = s.to_dense() if not s.orig_dense_tensor.is_sparse else s.to_coo_tensor()
+
+    def buffered_allreduce_fallback(self, grads=None, elements_per_buffer=500000000):
+        """All-reduce (average) the module's gradients bucket by bucket, per dtype; embedding gradients listed in
+        `sparse_tensor_module_names` travel as (indices, rows)."""
+        from .sparse_tensor import SparseTensor
+        if grads is None:
+            grads = []
+            sparse_names = set(getattr(self, "sparse_tensor_module_names", ()) or ())
+            for name, p in self.module.named_parameters():
+                if p.grad is None:
+                    continue
+                if name in sparse_names and not p.grad.is_sparse and p.grad.dim() == 2:
+                    st = SparseTensor(p.grad.data)
+                    st.orig_dense_tensor = p.grad
+                    grads.append(st)
+                else:
+                    grads.append(p.grad.data)
+        for kind, bucket in split_half_float_double_sparse(grads):
+            if kind == SparseTensor.type():
+                self.sparse_allreduce_no_retain(bucket)
+            else:
+                self.allreduce_no_retain(bucket, numel_per_bucket=elements_per_buffer)
+
+    def clip_fp32_gradients(self):
+        from .utils import clip_grad_norm_
+        clip_grad_norm_(parameters=self.module.parameters(), max_norm=self.gradient_clipping(), mpu=self.mpu)
+
+    # ---- further accessors
+    def is_elastic_model_parallel_supported(self):
+        return self.elasticity_enabled() and self._config.elasticity_config.get("version", 0.1) >= 0.2 \
+            if hasattr(self._config, "elasticity_config") else False
+
+    def flops_profiler_recompute_fwd_factor(self):
+        return getattr(self._config.flops_profiler_config, "recompute_fwd_factor", 0.0)
+
+    def autotuning_model_info_path(self):
+        return (self._config._param_dict.get("autotuning", {})).get("model_info_path")
+
+    def autotuning_profile_model_info(self):
+        at = self._config._param_dict.get("autotuning", {})
+        return bool(at.get("enabled", False) and (at.get("model_info") or {}).get("profile", False))
+
+    def quantize_training(self):
+        q = getattr(self, "quantizer", None)
+        return q is not None
+
+    def random_ltd_initialize(self):
+        return getattr(self, "random_ltd_scheduler", None)
+
+    def is_first_weights_partition_group(self):
+        """Does this rank belong to the first replica of the partitioned weights? (MiCS / hpZ replicate them)"""
+        opt = self.optimizer
+        replicas = getattr(opt, "mics_replica_group", None)
+        return True if replicas is None else dist.get_rank(replicas) == 0
+
+    @staticmethod
+    def load_moe_state_dict(checkpoint_path, tag, state_dict, old_moe_load, model=None, mpu=None, num_experts=1,
+                            checkpoint_engine=None):
+        """Merge the per-expert checkpoint files of `tag` into `state_dict` (see `_load_moe_experts`)."""
+        import glob
+        import os
+        for f in sorted(glob.glob(os.path.join(checkpoint_path, str(tag), "layer_*_expert_*_mp_rank_*_model_states.pt"))):
+            state_dict.update(torch.load(f, map_location="cpu", weights_only=True))
+        return state_dict
+
     def zero_grad(self):
         self.module.zero_grad(set_to_none=False)
 

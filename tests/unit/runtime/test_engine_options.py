@@ -175,3 +175,35 @@ def test_dataloader_worker_and_batch_defaults():
     assert dl.batch_size == 4 * n and dl.num_local_io_workers == 2 * n
     dl = DeepSpeedDataLoader(_Toy(32), 4, False, 0, None, num_local_io_workers=0)
     assert len(list(iter(dl))) == 8
+
+
+def _explicit_reductions(out):
+    """`buffered_allreduce_fallback` & co. on module gradients: averages dense grads per dtype bucket and the
+    embedding gradient as (indices, rows)."""
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    rank = dist.get_rank()
+    cfg = base_config(stage=0, lr=1e-2, mb=2)
+    cfg["sparse_gradients"] = True
+    eng, _, _, _ = ds.initialize(model=tiny_llama(), config=cfg)
+    torch.manual_seed(rank)
+    grads = {}
+    for n, p in eng.module.named_parameters():
+        p.grad = torch.randn_like(p)
+        if "embed_tokens" in n:
+            p.grad[5:] = 0          # only a few rows touched, as an embedding gradient would be
+        grads[n] = p.grad.clone()
+    every = [None, None]
+    dist.all_gather_object(every, grads)
+    eng.buffered_allreduce_fallback(elements_per_buffer=1000)    # small buffers: several buckets
+    for n, p in eng.module.named_parameters():
+        want = (every[0][n] + every[1][n]) / 2
+        torch.testing.assert_close(p.grad, want, rtol=1e-5, atol=1e-6, msg=n)
+    assert eng.all_gather_scalar(rank + 3) == [3, 4]
+    parts = eng.sparse_all_gather(torch.full((rank + 1, 2), float(rank)))
+    assert [p.shape[0] for p in parts] == [1, 2] and float(parts[1][0, 0]) == 1.0
+    assert eng.is_first_weights_partition_group() and eng.flops_profiler_recompute_fwd_factor() == 0.0
+
+
+def test_explicit_gradient_reductions(tmp_path):
+    run_distributed(_explicit_reductions, 2, None)
