@@ -163,6 +163,36 @@ class FlopsProfiler:
             out.close()
 
 
+def _aggregated(self, module_depth=-1, top_modules=1):
+    """{depth: [(module name, flops, seconds)]}: the `top_modules` largest modules of every depth by FLOPs."""
+    per_mod = self._module_flops()
+    by_name = {self._names[i]: d for i, d in self._durations.items() if i in self._names}
+    root = self.model.__class__.__name__
+    groups = defaultdict(list)
+    for name, f in per_mod.items():
+        if name == "Global":
+            continue
+        depth = name.count(".")
+        if module_depth >= 0 and depth > module_depth:
+            continue
+        short = name[len(root) + 1:] if name.startswith(root + ".") else name
+        groups[depth].append((name, f, by_name.get(short, by_name.get(name, 0.0))))
+    return {d: sorted(v, key=lambda r: -r[1])[:max(top_modules, 1)] for d, v in sorted(groups.items())}
+
+
+def _print_model_aggregated_profile(self, module_depth=-1, top_modules=1):
+    """Top modules per depth by FLOPs with their forward latency (reference `profiler.py:386-430`)."""
+    for depth, rows in _aggregated(self, module_depth, top_modules).items():
+        print(f"depth {depth}:")
+        print("    flops   - " + ", ".join(f"{n}: {flops_to_string(f)}" for n, f, _ in rows))
+        print("    latency - " + ", ".join(f"{n}: {duration_to_string(t)}" for n, _, t in rows))
+
+
+FlopsProfiler.print_model_aggregated_profile = _print_model_aggregated_profile
+FlopsProfiler.is_expert_tensor_parallelism_enabled = lambda self: any(
+    getattr(m, "enable_expert_tensor_parallelism", False) for m in self.model.modules())
+
+
 def get_model_profile(model, input_shape=None, args=None, kwargs=None, print_profile=True, detailed=True,
                       module_depth=-1, top_modules=1, warm_up=1, as_string=True, output_file=None, ignore_modules=None,
                       mode="forward"):

@@ -123,6 +123,22 @@ class OneCycle(_Sched):
         return [lo / (1 + self.decay_lr_rate * interval) for lo in self.min_lrs]
 
 
+    def get_mom(self):
+        """Momentum (beta1 / momentum) per parameter group at the current step, [(mom, beta2)] for Adam-style
+        groups; None when momentum is not cycled."""
+        if not self.cycle_momentum:
+            return None
+        it = self.last_batch_iteration + 1
+        out = []
+        if it < self.total:
+            s = self._scale()
+            for lo, hi in zip(self.min_moms, self.max_moms):
+                out.append((hi[0] - (hi[0] - lo[0]) * s, hi[1]))
+            return out
+        interval = (it - self.total) / self.decay_step_size if self.decay_step_size else 0
+        return [(hi[0] * (1 + self.decay_mom_rate * interval), hi[1]) for hi in self.max_moms]
+
+
 class WarmupLR(_Sched):
 
     def __init__(self, optimizer: Optimizer, warmup_min_lr=0.0, warmup_max_lr=0.001, warmup_num_steps=1000,
