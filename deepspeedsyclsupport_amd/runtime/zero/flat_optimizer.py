@@ -1521,8 +1521,8 @@ def model_to_params(model):
 def estimate_zero2_model_states_mem_needs(total_params, num_gpus_per_node=1, num_nodes=1, cpu_offload=True,
                                           additional_buffer_factor=1.5):
     """(host bytes per node, device bytes per GPU) for the model states under ZeRO-2 (reference
-    `stage_1_and_2.py:2396-2420`): 16-bit weights + gradients replicated (4 B / param), fp32 master + Adam moments
-    (16 B / param... 12 B of optimizer state + 4 B fp32 gradient) split over all GPUs or kept on the host."""
+    `stage_1_and_2.py:2396-2420`): 16-bit weights + gradients replicated (4 B / param); the fp32 master, the two
+    Adam moments and the fp32 gradient (16 B / param) split over all GPUs, or kept on the host."""
     total_gpus = num_nodes * num_gpus_per_node
     if cpu_offload:
         gpu_mem = 2 * total_params
