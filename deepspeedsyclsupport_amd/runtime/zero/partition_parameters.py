@@ -101,12 +101,6 @@ class ZeroParamType(Enum):
     REMOTE = 3     # lives on another device (host / NVMe) until fetched
 
 
-class ZeroParamStatus(Enum):
-    AVAILABLE = 1        # gathered: usable in compute
-    NOT_AVAILABLE = 2    # only this rank's partition is present
-    INFLIGHT = 3         # a gather is in progress
-
-
 class AllGatherHandle:
     """Completion handle of one parameter gather (reference `partition_parameters.py:620-640`). Gathers here are
     issued per flat group on the all-gather stream; the handle carries the event compute must wait for."""
