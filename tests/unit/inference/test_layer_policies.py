@@ -110,3 +110,21 @@ def test_policy_tables_and_readers():
     assert isinstance(cont, C.DS_LLAMAContainer)
     cfg = cont.create_ds_model_config()
     assert cfg.heads == 4 and cfg.num_kv == 2 and cfg.rotate_half and cfg.intermediate_size == 2 * H
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,policy", [("llama", "LLAMALayerPolicy"), ("gpt2", "HFGPT2LayerPolicy"),
+                                         ("bloom", "BLOOMLayerPolicy")])
+def test_hf_layers_replaced_through_policies_gpu(kind, policy):
+    """Per-layer injection on the device: the swapped-in layers run the HIP kernels in bf16."""
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd.module_inject import containers as C
+    m = tiny(kind, H=256).eval()
+    ids = torch.randint(0, m.config.vocab_size, (2, 24), generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        ref = m(ids, use_cache=False).logits.float()
+    eng = ds.init_inference(m, dtype=torch.bfloat16, injection_policy={_layer_cls(kind): getattr(C, policy)})
+    assert eng.policy_injected == m.config.num_hidden_layers
+    with torch.no_grad():
+        out = eng(ids.cuda(), use_cache=False).logits.float().cpu()
+    assert (out - ref).abs().max().item() < 0.05 * ref.abs().max().item() + 0.03
