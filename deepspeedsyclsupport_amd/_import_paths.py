@@ -27,7 +27,9 @@ PATHS = {
                                                      "iter_params": "iter_params",
                                                      "get_all_parameters": "get_all_parameters"})],
     "runtime.zero.parameter_offload": [("runtime.zero.coordinator", {"DeepSpeedZeRoOffload": "ParamCoordinator"})],
-    "runtime.zero.mics": [("runtime.zero", {"MiCS_Init": "MiCS_Init", "MiCS_Optimizer": "MiCS_Optimizer"})],
+    "runtime.zero.mics": [("runtime.zero", {"MiCS_Init": "MiCS_Init", "MiCS_Optimizer": "MiCS_Optimizer"}),
+                          ("runtime.zero.mics_utils", {"MiCS_CommGroups": "MiCS_CommGroups",
+                                                       "create_mics_comm_groups": "create_mics_comm_groups"})],
     "runtime.bf16_optimizer": [("runtime.zero.flat_optimizer", {"BF16_Optimizer": "BF16_Optimizer"})],
     "runtime.fp16.fused_optimizer": [("runtime.zero.flat_optimizer", {"FP16_Optimizer": "FP16_Optimizer"})],
     "runtime.fp16.unfused_optimizer": [("runtime.zero.flat_optimizer", {"FP16_UnfusedOptimizer": "FP16_Optimizer"})],
@@ -78,7 +80,6 @@ PATHS = {
     "runtime.data_pipeline.data_sampling.utils": [("runtime.data_pipeline.data_sampling.indexed_dataset", "*"),
                                                   ("runtime.data_pipeline.data_sampling.data_analyzer",
                                                    {"split_index": "split_index", "split_dataset": "split_dataset"})],
-    "runtime.zero.mics_utils": [("runtime.zero", "*")],
     "autotuning.scheduler": [("autotuning.autotuner", {"ResourceManager": "ResourceManager"})],
     "monitor.utils": [("monitor.monitor", {"check_tb_availability": "check_tb_availability",
                                            "check_wandb_availability": "check_wandb_availability"})],

@@ -835,38 +835,16 @@ class FlatZeroOptimizer(ZeROOptimizer):
         S = int(getattr(self.zc, "mics_shard_size", -1) or -1) if self.zc is not None else -1
         if S <= 1 or S >= self.dp or self.stage < 1:
             return
-        assert self.dp % S == 0, f"mics_shard_size {S} must divide the data-parallel size {self.dp}"
+        from .mics_utils import create_mics_comm_groups
         ranks = dist.get_all_ranks_from_group(self.dp_group) if self.dp != self.world else list(range(self.world))
-        me = dist.get_rank()
-        for i in range(self.dp // S):
-            grp = ranks[i * S:(i + 1) * S]
-            g = dist.new_group(grp)
-            if me in grp:
-                self.mics_shard_group = g
-        for j in range(S):
-            grp = ranks[j::S]
-            g = dist.new_group(grp)
-            if me in grp:
-                self.mics_replica_group = g
-        self.mics_replicas = self.dp // S
-        # mics_hierarchical_params_gather: a shard group that spans nodes gathers in two levels
-        self.mics_hier = None
-        node = int(os.environ.get("DS_NODE_SIZE", 0)) or max(get_accelerator().device_count(), 1)
-        if bool(getattr(self.zc, "mics_hierarchical_params_gather", False)) and S > node and S % node == 0:
-            intra = inter = None
-            for i in range(self.dp // S):
-                grp = ranks[i * S:(i + 1) * S]
-                for a in range(S // node):            # the ranks of one node inside this shard group
-                    sub = grp[a * node:(a + 1) * node]
-                    g = dist.new_group(sub)
-                    if me in sub:
-                        intra = g
-                for b in range(node):                 # one local index across the shard group's nodes
-                    sub = grp[b::node]
-                    g = dist.new_group(sub)
-                    if me in sub:
-                        inter = g
-            self.mics_hier = (intra, inter)
+        cg = create_mics_comm_groups(S, self.dp_group, bool(getattr(self.zc, "mics_hierarchical_params_gather",
+                                                                    False)), ranks=ranks)
+        self.mics_groups = cg
+        self.mics_shard_group, self.mics_replica_group = cg.param_shard_group, cg.param_repli_group
+        self.mics_replicas = cg.param_repli_size
+        # a shard group that spans nodes gathers its parameters in two levels
+        if cg.param_intra_node_group is not None:
+            self.mics_hier = (cg.param_intra_node_group, cg.param_inter_node_shard_group)
 
     def _grad_items(self):
         """[(og, moff, n, grad_1d, lp_1d, scale)] covering every DEVICE-resident master element that has a gradient
