@@ -248,3 +248,18 @@ def test_accelerator_builder_and_legacy_surface():
     assert a.LongTensor([1]).dtype == torch.int64 and a.BFloat16Tensor([1]).dtype == torch.bfloat16
     assert a.memory_cached() == a.memory_reserved() and a.max_memory_cached() == a.max_memory_reserved()
     assert a.amp() is torch.amp and not a.is_triton_supported() and "RCCL" in a.export_envs()
+
+
+def test_config_key_constants_follow_the_defaults_tables():
+    """`compression.constants` is built from the defaults tables the config parser uses; the data-pipeline key
+    names are served under the reference's path."""
+    from deepspeedsyclsupport_amd.compression import constants as cc
+    from deepspeedsyclsupport_amd.compression.config import SHARED_DEFAULTS
+    from deepspeedsyclsupport_amd.runtime.data_pipeline import constants as dc
+    assert cc.WEIGHT_QUANTIZATION == "weight_quantization" and cc.WEIGHT_QUANTIZE_GROUPS == "quantize_groups"
+    assert cc.WEIGHT_QUANTIZE_GROUPS_DEFAULT == SHARED_DEFAULTS["weight_quantization"]["quantize_groups"]
+    assert cc.WEIGHT_QUANTIZE_STOCHASTIC_ROUNDING == "stochastic" and cc.ACTIVATION_QUANTIZE_RANGE_STATIC == "static"
+    assert cc.SPARSE_PRUNING_METHOD_SNIP_MOMENTUM == "snip_momentum" and cc.HEAD_PRUNING_NUM_HEADS == "num_heads"
+    assert cc.KEEP_NUMBER_LAYER == "keep_number_layer"
+    assert dc.RANDOM_LTD_SCHEDULER == "random_ltd_schedule" and dc.RANDOM_LTD_ENABLED_DEFAULT is False
+    assert dc.CURRICULUM_LEARNING_SCHEDULE_FIXED_ROOT == "fixed_root" and dc.DATA_EFFICIENCY_SEED_DEFAULT == 1234
