@@ -108,6 +108,9 @@ PATHS = {
     **{f"module_inject.containers.{f}": [("module_inject.containers", "*")]
        for f in ("base", "base_moe", "bert", "bloom", "clip", "distil_bert", "gpt2", "gptj", "gptneo", "gptneox",
                  "internlm", "llama", "llama2", "megatron_gpt", "megatron_gpt_moe", "opt", "unet", "vae")},
+    **{f"module_inject.containers.features.{f}": [("module_inject.container_features", "*")]
+       for f in ("gated_mlp", "hybrid_engine", "hybrid_megatron", "megatron", "meta_tensor", "split_qkv")},
+    "module_inject.containers.features": [("module_inject.container_features", "*")],
     "module_inject.replace_policy": [("module_inject.containers", {"replace_policies": "replace_policies",
                                                                   "generic_policies": "generic_policies"})],
     "module_inject.utils": [("module_inject.containers", {"policy_to_ds_container": "policy_to_ds_container"})],
@@ -268,6 +271,11 @@ def _virtual_packages():
     return _VIRTUAL
 
 
+def _has_children(rel):
+    """A served path that other served paths lie below (the reference's `__init__.py` re-exports)."""
+    return any(k.startswith(rel + ".") for k in list(PATHS) + list(GENERATED))
+
+
 class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
 
     def find_spec(self, fullname, path=None, target=None):
@@ -275,7 +283,7 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
             return None
         rel = fullname[len(_PKG) + 1:]
         if rel in PATHS or rel in GENERATED:
-            return importlib.machinery.ModuleSpec(fullname, self)
+            return importlib.machinery.ModuleSpec(fullname, self, is_package=_has_children(rel))
         if rel in _virtual_packages():
             return importlib.machinery.ModuleSpec(fullname, self, is_package=True)
         return None
@@ -295,6 +303,8 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
             module.__doc__ = f"Reference package `deepspeed.{rel}` (paths below it: `{_PKG}/_import_paths.py`)."
             return
         module.__doc__ = f"Reference import path `deepspeed.{rel}` (see `{_PKG}/_import_paths.py`)."
+        if _has_children(rel):
+            module.__path__ = []
         for real, names in PATHS[rel]:
             src = importlib.import_module(f"{_PKG}.{real}")
             if names == "*":
