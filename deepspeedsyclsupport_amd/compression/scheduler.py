@@ -9,6 +9,7 @@ reaches its `schedule_offset`; after that
 import torch
 
 from .basic_layer import fake_quant
+from .config import TECHNIQUES
 from .helper import recursive_getattr
 
 
@@ -69,9 +70,11 @@ class compression_scheduler:
         else:
             m.update_masks()
 
-    def step(self, step_zero_check=None):
-        step = self._step if step_zero_check is None else int(step_zero_check)
+    def _check(self, techs, step):
+        """Switch on / advance the given techniques at training step `step`."""
         for (tech, n, shared, params, related) in self._plan():
+            if tech not in techs:
+                continue
             m = recursive_getattr(self.model, n)
             key = (tech, n)
             if key not in self.enabled:
@@ -89,4 +92,56 @@ class compression_scheduler:
                 bits = getattr(m, "wq_bits", getattr(m, "wq_target_bits", 8))
                 with torch.no_grad():
                     m.weight.copy_(fake_quant(m.weight, bits, m.wq_groups, m.wq_symmetric))
+
+    def step(self, step_zero_check=None):
+        step = self._step if step_zero_check is None else int(step_zero_check)
+        self._check(TECHNIQUES, step)
         self._step = step + 1
+
+    # ---- the reference's per-technique entry points (`compression/scheduler.py:66-160`)
+    @property
+    def training_steps(self):
+        return self._step
+
+    @training_steps.setter
+    def training_steps(self, v):
+        self._step = int(v)
+
+    def make_init(self):
+        """{technique: {"enabled", "shared_parameters", "different_groups": [[group, [module names], params]]}} —
+        the plan `init_compression` attached to the model, regrouped per technique."""
+        out = {}
+        for tech in TECHNIQUES:
+            shared = self.cc[tech]["shared_parameters"]
+            groups = {}
+            for (t, n, _, params, _) in self._plan():
+                if t == tech:
+                    groups.setdefault(id(params), [None, [], params])[1].append(n)
+            names = list(self.cc[tech]["different_groups"])
+            rows = list(groups.values())
+            for i, row in enumerate(rows):
+                row[0] = names[i] if i < len(names) else f"group_{i}"
+            out[tech] = {"enabled": shared["enabled"], "shared_parameters": shared, "different_groups": rows}
+        self.different_compression_methods = out
+        return out
+
+    def check_weight_quantization(self):
+        self._check(("weight_quantization", ), self._step)
+
+    def check_activation_quantization(self):
+        self._check(("activation_quantization", ), self._step)
+
+    def check_sparse_pruning(self):
+        self._check(("sparse_pruning", ), self._step)
+
+    def check_head_pruning(self):
+        self._check(("head_pruning", ), self._step)
+
+    def check_row_pruning(self):
+        self._check(("row_pruning", ), self._step)
+
+    def check_channel_pruning(self):
+        self._check(("channel_pruning", ), self._step)
+
+    def check_all_modules(self):
+        self._check(TECHNIQUES, self._step)

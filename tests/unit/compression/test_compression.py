@@ -216,6 +216,31 @@ def test_gradual_sparse_and_inplace_weight_quant_schedule():
     assert m.head.weight.reshape(-1).unique().numel() <= 16  # quantised in place by the scheduler
 
 
+def test_scheduler_per_technique_checks():
+    """The reference's entry points: `check_<technique>()` advances one technique at `training_steps`,
+    `make_init()` regroups the plan per technique."""
+    from deepspeedsyclsupport_amd.compression import compression_scheduler
+    m = MLP()
+    cfg = _cfg(sparse_pruning={"shared_parameters": {"enabled": True, "method": "l1", "schedule_offset": 3},
+                               "different_groups": {"sp": {"params": {"dense_ratio": 0.5}, "modules": ["layers.0.0"]}}},
+               row_pruning={"shared_parameters": {"enabled": True, "method": "l1", "schedule_offset": 0},
+                            "different_groups": {"rp": {"params": {"dense_ratio": 0.5}, "modules": ["layers.1.0"]}}})
+    init_compression(m, cfg)
+    sch = compression_scheduler(m, cfg)
+    table = sch.make_init()
+    assert table["sparse_pruning"]["enabled"] and table["sparse_pruning"]["different_groups"][0][:2] == \
+        ["sp", ["layers.0.0"]]
+    assert table["row_pruning"]["different_groups"][0][1] == ["layers.1.0"] and \
+        table["head_pruning"]["different_groups"] == []
+    sch.check_sparse_pruning()                       # step 0 < offset 3: nothing
+    assert not getattr(m.layers[0][0], "sparse_pruning_enabled", False)
+    sch.check_row_pruning()
+    assert m.layers[1][0].row_pruning_enabled and not getattr(m.layers[0][0], "sparse_pruning_enabled", False)
+    sch.training_steps = 3
+    sch.check_all_modules()
+    assert m.layers[0][0].sparse_pruning_enabled and sch.training_steps == 3
+
+
 def _tp_run(out):
     import torch.distributed as dist
     from deepspeedsyclsupport_amd.compression import ColumnParallelLinear_Compress, RowParallelLinear_Compress
