@@ -1511,7 +1511,7 @@ _ZERO_ACCESSORS = {
     "zero_model_persistence_threshold": "model_persistence_threshold",
     "zero_max_live_parameters": "max_live_parameters", "zero_max_reuse_distance": "max_reuse_distance",
     "zero_gather_16bit_weights_on_model_save": "gather_16bit_weights_on_model_save",
-    "zero_ignore_unused_parameters": "ignore_unused_parameters", "zero_legacy_stage1": "legacy_stage1",
+    "zero_ignore_unused_parameters": "ignore_unused_parameters", "zero_legacy_stage1": "legacy_stage1", "zero_grad_hooks": "grad_hooks",
     "zero_round_robin_gradients": "round_robin_gradients", "zero_load_from_fp32_weights": "load_from_fp32_weights",
     "zero_elastic_checkpoint": "elastic_checkpoint", "zero_hpz_partition_size": "zero_hpz_partition_size",
     "zero_quantized_weights": "zero_quantized_weights", "zero_quantized_gradients": "zero_quantized_gradients",

@@ -50,6 +50,7 @@ class DeepSpeedZeroConfig(DeepSpeedConfigModel):
     stage3_gather_fp16_weights_on_model_save: bool = False
     ignore_unused_parameters: bool = True
     legacy_stage1: bool = False
+    grad_hooks: bool = True
     round_robin_gradients: bool = False
     zero_hpz_partition_size: int = Field(1, ge=0)
     zero_quantized_weights: bool = False

@@ -585,6 +585,14 @@ class FlatZeroOptimizer(ZeROOptimizer):
             if g.mode == self.PRESET:
                 g.grad_flat = torch.zeros(g.padded, dtype=self.dtype, device=self.device)
                 self._point_grads(g)
+        # `grad_hooks: false` (reference `zero/config.py: grad_hooks`, stages 1/2): no per-parameter hooks fire
+        # inside autograd; the whole pass is folded into the flat buffers and reduced in `backward_epilogue`
+        self.grad_hooks = bool(getattr(self.zc, "grad_hooks", True)) if self.zc is not None else True
+        if not self.grad_hooks:
+            if self.stage == 3:
+                raise ValueError("zero_optimization.grad_hooks=false is for stages 0-2: stage 3 releases gathered "
+                                 "parameters from the gradient hooks")
+            return
         for p in self.opt_params:
             g, _ = self.param_group[id(p)]
             if g.mode != self.LOCAL or self.coordinator_needed() or g.pieces:
@@ -769,6 +777,11 @@ class FlatZeroOptimizer(ZeROOptimizer):
     @instrument_w_nvtx
     def backward_epilogue(self):
         """Flush groups whose params got no grad this pass (unused params count as zero) and join streams."""
+        if not self.grad_hooks:
+            for p in reversed(self.opt_params):
+                g, _ = self.param_group[id(p)]
+                if p.grad is not None and (g.mode != self.LOCAL or g.pieces):
+                    self._grad_ready_hook(p)
         if not self.ignore_unused:
             names = None
             for g in self.groups:

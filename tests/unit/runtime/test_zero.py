@@ -69,6 +69,50 @@ def test_zero_matches_torch(stage, world, gas, tmp_path):
             torch.testing.assert_close(got["sd"][k].float(), v.float(), rtol=1e-3, atol=2e-4, msg=k)
 
 
+def _no_hooks_run(stage, world, steps, gas, out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    rank = dist.get_rank()
+    cfg = base_config(stage=stage, lr=1e-2, mb=2, gas=gas, clip=1.0)
+    cfg["zero_optimization"]["grad_hooks"] = False
+    eng, _, _, _ = ds.initialize(model=tiny_llama(), config=cfg)
+    assert eng.zero_grad_hooks() is False and eng.optimizer._hooks == []
+    data = random_tokens(steps * gas, 2, 16, seed=100 + rank)
+    losses = []
+    for s in range(steps):
+        tot = torch.zeros(())
+        for a in range(gas):
+            x = data[s * gas + a]
+            loss = eng(x, labels=x)
+            eng.backward(loss)
+            eng.step()
+            tot += loss.detach() / gas
+        dist.all_reduce(tot)
+        losses.append(float(tot) / world)
+    if rank == 0:
+        torch.save({"losses": losses}, out)
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+def test_zero_without_grad_hooks(stage, tmp_path):
+    """`grad_hooks: false`: no autograd hooks; gradients are folded and reduced after the backward pass, with the
+    same numerics."""
+    world, steps, gas = 2, 3, 2
+    out = str(tmp_path / "res.pt")
+    run_distributed(_no_hooks_run, world, stage, world, steps, gas, out)
+    got = torch.load(out, weights_only=True)["losses"]
+    ref, _ = _reference_losses(world, steps, gas, 2, 16, 1e-2, 1.0)
+    assert got == pytest.approx(ref, rel=1e-4, abs=1e-5), (got, ref)
+
+
+def test_grad_hooks_false_rejected_for_stage3():
+    import deepspeedsyclsupport_amd as ds
+    cfg = base_config(stage=3, lr=1e-2, mb=2)
+    cfg["zero_optimization"]["grad_hooks"] = False
+    with pytest.raises(ValueError, match="grad_hooks"):
+        ds.initialize(model=tiny_llama(), config=cfg)
+
+
 def _zeropp_run(world, zpp, out):
     import deepspeedsyclsupport_amd as ds
     from deepspeedsyclsupport_amd import comm as dist
