@@ -271,6 +271,106 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
         self._t_generate += self._t_last
         return out
 
+    # ------------------------------------------------------------------------------------------ per-layer containers
+    # Architectures without a whole-model converter can still run their transformer layers fused: every client
+    # layer a policy of `module_inject.containers.replace_policies` matches gets a hybrid container (reference
+    # `runtime/hybrid_engine.py:84-160, 280-330`), and `fused_layers()` swaps the layers' forwards for the fused
+    # ones while it is open.
+    def populate_all_inference_policies(self):
+        from ..module_inject.containers import replace_policies
+        self.inference_policies = {}
+        for pol in replace_policies:
+            try:
+                pol(None)            # policies resolve their client layer class on first construction
+            except Exception:
+                pass
+            classes = pol._orig_layer_class
+            for c in (classes if isinstance(classes, (list, tuple)) else [classes]):
+                if c is not None:
+                    self.inference_policies[c] = pol
+        return self.inference_policies
+
+    def new_inference_container(self, orig_layer, policy_cls, layer_id):
+        from ..inference.config import DeepSpeedInferenceConfig
+        from ..module_inject import containers as C
+        from ..module_inject.container_features import HybridEngineContainer
+        policy = policy_cls(orig_layer, inference=True)
+        dtype = self._dtype() if self._dtype() in (torch.bfloat16, torch.float16) else torch.float32
+        base = C.BaseTransformerContainer
+        for cls in type(policy).__mro__:
+            if cls in C._CONTAINERS:
+                base = C._CONTAINERS[cls]
+                break
+        kind = type("Hybrid" + base.__name__, (HybridEngineContainer, base), {})
+        cfg = DeepSpeedInferenceConfig(dtype=dtype, max_out_tokens=self.hcfg.max_out_tokens)
+        cont = kind(policy=policy, config=cfg, model_config=getattr(self.module, "config", None), layer_id=layer_id,
+                    child=orig_layer)
+        cont.create_ds_model_config()
+        cont.create_module()
+        return cont
+
+    def create_inference_containers(self, module=None, layer_id=0):
+        module = self.module if module is None else module
+        for child in module.children():
+            pol = self.inference_policies.get(type(child))
+            if pol is not None:
+                self._inference_containers.append(self.new_inference_container(child, pol, layer_id))
+                self._orig_modules.append(child)
+                self._orig_fwds.append(child.forward)
+                layer_id += 1
+            else:
+                layer_id = self.create_inference_containers(child, layer_id)
+        return layer_id
+
+    def create_inference_module(self):
+        self._inference_containers, self._orig_modules, self._orig_fwds = [], [], []
+        self.populate_all_inference_policies()
+        self.create_inference_containers(self.module)
+        self.lora_params = [c.get_lora_params() for c in self._inference_containers]
+        return len(self._inference_containers)
+
+    def fused_layers(self):
+        """Context manager: refresh every layer container from the (just trained) client weights and run the
+        client layers through their fused counterparts until it closes."""
+        import contextlib
+        from ..module_inject.containers import _InjectedLayer
+
+        @contextlib.contextmanager
+        def ctx():
+            if not getattr(self, "_inference_containers", None):
+                self.create_inference_module()
+            with self._gathered():
+                for c in self._inference_containers:
+                    c.transform_for_inference()
+            try:
+                for c, m in zip(self._inference_containers, self._orig_modules):
+                    m.forward = _InjectedLayer(c.module, c.policy.return_tuple).forward
+                yield self._inference_containers
+            finally:
+                for m, f in zip(self._orig_modules, self._orig_fwds):
+                    m.forward = f
+                if self.hcfg.release_inference_cache:
+                    for c in self._inference_containers:
+                        c.release_memory()
+
+        return ctx()
+
+    def retake_inference_cache(self):
+        """Bring back what `release_inference_cache` dropped (the KV cache of the whole-model path is re-allocated
+        by the next generate on its own)."""
+        for c in getattr(self, "_inference_containers", []):
+            if c._released:
+                c.reset_params()
+
+    def unfuse_lora_weight_non_pinned(self):
+        with self._gathered():
+            self.unfuse_lora_weight()
+
+    def convert_to_linear_transposed(self, model):
+        """The reference re-wraps nn.Linear to hold transposed weights for its GEMMs; the GEMMs here take the
+        [out, in] weights as stored, so there is nothing to convert."""
+        return model
+
     def eval(self):
         self.module.eval()
         return self

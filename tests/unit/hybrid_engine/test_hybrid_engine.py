@@ -98,3 +98,50 @@ def test_hybrid_generate_tracks_training(stage, lora, tp, tmp_path):
     results = torch.load(out, weights_only=True)
     for got, ref in results:
         assert torch.equal(got, ref)
+
+
+def _per_layer(out):
+    import deepspeedsyclsupport_amd as ds
+    from ..inference.test_inference import tiny
+    model = tiny("gpt2")
+    cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}},
+           "zero_optimization": {"stage": 1},
+           "hybrid_engine": {"enabled": True, "max_out_tokens": 64, "release_inference_cache": True}}
+    eng, _, _, _ = ds.initialize(model=model, config=cfg)
+    assert eng.create_inference_module() == model.config.num_hidden_layers
+    assert type(eng._orig_modules[0]) in eng.inference_policies
+    ids = torch.randint(0, model.config.vocab_size, (2, 10), generator=torch.Generator().manual_seed(5))
+    diffs, moved = [], []
+    prev = None
+    for step in range(2):
+        loss = eng(input_ids=ids, labels=ids).loss
+        eng.backward(loss)
+        eng.step()
+        eng.eval()
+        with torch.no_grad():
+            ref = eng.module(ids, use_cache=False).logits.float()
+            with eng.fused_layers() as conts:
+                assert all(c.module.layer.qkv_w.numel() for c in conts)
+                got = eng.module(ids, use_cache=False).logits.float()
+            # forwards are the client's again, and the inference copies were released
+            again = eng.module(ids, use_cache=False).logits.float()
+        eng.train()
+        assert all(c._released and c.module.layer.qkv_w.numel() == 0 for c in eng._inference_containers)
+        diffs.append(float((got - ref).abs().max()))
+        torch.testing.assert_close(again, ref)
+        if prev is not None:
+            moved.append(float((ref - prev).abs().max()))
+        prev = ref
+    eng.retake_inference_cache()
+    assert all(not c._released and c.module.layer.qkv_w.numel() for c in eng._inference_containers)
+    assert eng.convert_to_linear_transposed(model) is model
+    torch.save({"diffs": diffs, "moved": moved}, out)
+
+
+def test_per_layer_containers_track_training(tmp_path):
+    """Layer containers built from `replace_policies`: inside `fused_layers()` the client layers run fused on the
+    freshly trained weights; outside, the client forwards are back and the inference copies are released."""
+    out = str(tmp_path / "r.pt")
+    run_distributed(_per_layer, 1, out)
+    r = torch.load(out, weights_only=True)
+    assert max(r["diffs"]) < 2e-3 and r["moved"][0] > 10 * max(r["diffs"]), r
