@@ -88,6 +88,7 @@ class InferenceEngine(torch.nn.Module):
                     for layer_cls, policy_cls in by_policy.items())
             if by_names:
                 AutoTP(model, self.mp_group, self.tp_size, self.tp_rank, injection_policy=by_names).apply()
+                self._patch_head_indexed_bias(model)
             self.module = model.to(self.device)
             if self.dtype in (torch.float16, torch.bfloat16, torch.float32):
                 self.module = self.module.to(self.dtype)
@@ -121,11 +122,49 @@ class InferenceEngine(torch.nn.Module):
             if self.tp_size > 1:
                 from ..module_inject.auto_tp import AutoTP
                 AutoTP(model, self.mp_group, self.tp_size, self.tp_rank).apply()
+                self._patch_head_indexed_bias(model)
             self.module = model.to(self.device)
             if self.dtype in (torch.float16, torch.bfloat16, torch.float32):
                 self.module = self.module.to(self.dtype)
         self.module.eval()
         log_dist(f"InferenceEngine: injected={self.injected} tp={self.tp_size} dtype={self.dtype}", ranks=[0])
+
+    # ---- models whose attention bias is indexed by head: after the heads are divided over the TP ranks the
+    # model's own builder must return this rank's heads only (reference `inference/engine.py:105-110, 214-236`)
+    def _patch_head_indexed_bias(self, model):
+        if self.tp_size <= 1:
+            return
+        from ..module_inject.auto_tp_model_utils import set_tp_group
+        set_tp_group(self.mp_group, self.tp_size, self.tp_rank)
+        self.module = model
+        self.build_alibi_tensor()
+        self.build_attn_bias()
+
+    def remove_mask_prepare_for_bloom(self):
+        """Old HF BLOOM expands the padding mask itself; the fused layers take the [batch, seq] mask as it is."""
+        tr = getattr(self.module, "transformer", None)
+        if tr is not None and hasattr(tr, "_prepare_attn_mask"):
+            tr._prepare_attn_mask = lambda attention_mask, *args, **kwargs: attention_mask
+
+    def build_alibi_tensor(self):
+        from ..module_inject import auto_tp_model_utils as U
+        tr = getattr(self.module, "transformer", None)
+        if tr is not None and hasattr(tr, "build_alibi_tensor"):            # BLOOM
+            tr.build_alibi_tensor = U.build_bloom_alibi_tensor
+        if tr is not None and hasattr(tr, "build_mpt_alibi_tensor"):        # MPT
+            tr.build_mpt_alibi_tensor_orig = tr.build_mpt_alibi_tensor
+            type(tr).build_mpt_alibi_tensor = U.build_mpt_alibi_tensor
+        inner = getattr(self.module, "model", None)
+        if inner is not None and hasattr(inner, "get_alibi_mask"):          # Baichuan
+            inner.get_alibi_mask_orig = inner.get_alibi_mask
+            type(inner).get_alibi_mask = U.get_alibi_mask
+
+    def build_attn_bias(self):
+        from ..module_inject import auto_tp_model_utils as U
+        tr = getattr(self.module, "transformer", None)
+        if tr is not None and hasattr(tr, "_attn_bias"):                    # MPT (remote-code versions)
+            tr._attn_bias_orig = tr._attn_bias
+            type(tr)._attn_bias = U.build_mpt_atten_bias_tensor
 
     def _apply_decode_layout(self, config):
         """`decode_layout` of the inference config: a shuffled copy of the bf16 projection weights for batched

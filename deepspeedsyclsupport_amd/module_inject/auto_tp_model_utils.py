@@ -21,10 +21,23 @@ def _alibi_slopes(num_heads, device):
     return slopes
 
 
+_TP = {"group": None, "size": None, "rank": None}
+
+
+def set_tp_group(group=None, size=None, rank=None):
+    """The tensor-parallel group whose ranks share the heads (default: every rank of the job)."""
+    _TP.update(group=group, size=size, rank=rank)
+
+
 def _my_heads(num_heads):
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if _TP["size"] is not None:
+        world, rank = _TP["size"], _TP["rank"]
+    elif not dist.is_initialized() or dist.get_world_size() == 1:
         return 0, num_heads
-    world, rank = dist.get_world_size(), dist.get_rank()
+    else:
+        world, rank = dist.get_world_size(), dist.get_rank()
+    if world == 1:
+        return 0, num_heads
     per = num_heads // world
     return rank * per, (rank + 1) * per
 

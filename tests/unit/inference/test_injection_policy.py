@@ -124,3 +124,33 @@ def test_bloom_alibi_matches_transformers():
     for heads in (8, 12):
         torch.testing.assert_close(build_bloom_alibi_tensor(mask, heads, torch.float32),
                                    build_alibi_tensor(mask, heads, torch.float32))
+
+
+def _bloom_tp(out):
+    import deepspeedsyclsupport_amd as ds
+    from deepspeedsyclsupport_amd import comm as dist
+    from .test_inference import tiny
+    dist.init_distributed("gloo")
+    m = tiny("bloom").eval()
+    ids = torch.randint(0, m.config.vocab_size, (2, 9), generator=torch.Generator().manual_seed(1))
+    mask = torch.ones_like(ids)
+    mask[1, :3] = 0                                    # left padding: ALiBi positions follow the mask
+    with torch.no_grad():
+        ref = m(ids, attention_mask=mask, use_cache=False).logits
+    eng = ds.init_inference(m, dtype=torch.float32, tensor_parallel={"tp_size": 2})
+    assert "build_alibi_tensor" in vars(eng.module.transformer)      # the per-rank builder is in place
+    with torch.no_grad():
+        got = eng.module(ids, attention_mask=mask, use_cache=False).logits
+    if dist.get_rank() == 0:
+        torch.save({"ref": ref, "got": got}, out)
+
+
+def test_auto_tp_bloom_alibi_per_rank(tmp_path):
+    """HF BLOOM under AutoTP (no kernel injection), 2 ranks: each rank's attention gets the ALiBi rows of its own
+    heads, and the logits equal the unsharded model's."""
+    from ..common import run_distributed
+    out = str(tmp_path / "r.pt")
+    run_distributed(_bloom_tp, 2, out)
+    r = torch.load(out, weights_only=True)
+    torch.testing.assert_close(r["got"][0], r["ref"][0], rtol=2e-4, atol=2e-4)
+    torch.testing.assert_close(r["got"][1, 3:], r["ref"][1, 3:], rtol=2e-4, atol=2e-4)
